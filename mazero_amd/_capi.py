@@ -1,0 +1,117 @@
+"""ctypes binding of the C-ABI declared in include/mzmcts.h.
+
+`bind(lib)` declares argument/return types on any shared library exporting that ABI.  The product
+loads its own HIP library through `mazero_amd._lib.load()`; the tests use the same binder on the
+oracle libraries (oracle/_ref/libmzref.so, oracle/_build/libmzport.so) to drive all backends
+through one code path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+MZ_OK, MZ_ERR_ARG, MZ_ERR_RUNTIME, MZ_ERR_DEVICE, MZ_ERR_UNSUPPORTED = 0, 1, 2, 3, 4
+MZ_MEM_HOST, MZ_MEM_DEVICE = 0, 1
+
+# enum mz_field (include/mzmcts.h), in the order of the cytree.pyx readbacks (cytree.pyx:111-241)
+FIELDS = {
+    "actions": 0,
+    "visit_count": 1,
+    "pred_probs": 2,
+    "beta": 3,
+    "beta_hat": 4,
+    "priors": 5,
+    "imp_ratio": 6,
+    "pred_values": 7,
+    "mcts_values": 8,
+    "rewards": 9,
+    "qvalues": 10,
+}
+INT_FIELDS = {"actions", "visit_count"}
+
+STATS = [
+    "selects",
+    "path_edges",
+    "scored",
+    "expands",
+    "new_children",
+    "backup_nodes",
+    "entries_read",
+    "entries_written",
+    "minmax_nodes",
+]
+
+EXPORTS = [
+    "mz_last_error",
+    "mz_abi_version",
+    "mz_backend",
+    "mz_create",
+    "mz_destroy",
+    "mz_set_stream",
+    "mz_synchronize",
+    "mz_prepare",
+    "mz_select",
+    "mz_expand_backup",
+    "mz_expand_backup_select",
+    "mz_gather_rows",
+    "mz_get_roots_values",
+    "mz_get_roots_marginal_visit_count",
+    "mz_get_roots_marginal_priors",
+    "mz_get_num_children_of_root",
+    "mz_get_root_sampled",
+    "mz_max_children",
+    "mz_get_roots_sampled_padded",
+    "mz_get_stats",
+    "mz_print",
+]
+
+_p = C.c_void_p
+_i = C.c_int
+_f = C.c_float
+_i64 = C.c_int64
+
+
+def bind(lib: C.CDLL) -> C.CDLL:
+    sig = {
+        "mz_last_error": (C.c_char_p, []),
+        "mz_abi_version": (_i, []),
+        "mz_backend": (C.c_char_p, []),
+        "mz_create": (_i, [_i, _i, _i, _i, _i, _f, C.c_uint32, _f, _f, _i, C.POINTER(_p)]),
+        "mz_destroy": (_i, [_p]),
+        "mz_set_stream": (_i, [_p, _p]),
+        "mz_synchronize": (_i, [_p]),
+        "mz_prepare": (_i, [_p, _p, _p, _p, _p, _i, _f, _p, _i]),
+        "mz_select": (_i, [_p, _f, _f, _f, _p, _p, _p, _i]),
+        "mz_expand_backup": (_i, [_p, _i, _f, _i, _p, _p, _p, _p, _i]),
+        "mz_expand_backup_select": (
+            _i,
+            [_p, _i, _f, _i, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _i64, _i64, _p],
+        ),
+        "mz_gather_rows": (_i, [_p, _p, _i64, _i64, _p, _p]),
+        "mz_get_roots_values": (_i, [_p, _p, _i]),
+        "mz_get_roots_marginal_visit_count": (_i, [_p, _p, _i]),
+        "mz_get_roots_marginal_priors": (_i, [_p, _p, _i]),
+        "mz_get_num_children_of_root": (_i, [_p, _i, _p]),
+        "mz_get_root_sampled": (_i, [_p, _i, _i, _f, _p]),
+        "mz_max_children": (_i, [_p, _p]),
+        "mz_get_roots_sampled_padded": (_i, [_p, _i, _f, _p, _p, _i]),
+        "mz_get_stats": (_i, [_p, _p]),
+        "mz_print": (_i, [_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+class MZError(RuntimeError):
+    """Raised for a non-zero mz_* status; a RuntimeError like the reference's `except +`."""
+
+
+def check(lib: C.CDLL, rc: int, what: str) -> None:
+    if rc != MZ_OK:
+        msg = lib.mz_last_error()
+        msg = msg.decode() if msg else ""
+        if rc == MZ_ERR_ARG:
+            raise ValueError(f"{what}: {msg}")
+        raise MZError(f"{what}: {msg}" if msg else f"{what}: status {rc}")

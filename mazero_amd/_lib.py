@@ -1,0 +1,38 @@
+"""Loader of the product library mazero_amd/_build/libmzmcts.so.
+
+There is no fallback: if the HIP library is missing or cannot be loaded, this raises.  torch is
+imported first when available so that the HIP runtime torch ships (libamdhip64.so.7, same
+soname) is the one the library binds to -- one HIP runtime per process.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from . import _capi
+from .build import LIB
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        try:
+            import torch  # noqa: F401  (plumbing: share torch's HIP runtime)
+        except Exception:
+            pass
+        if not os.path.exists(LIB):
+            raise RuntimeError(
+                f"MI355X library not built: {LIB} is missing (run `python -m mazero_amd.build` "
+                "or __graft_entry__.build())"
+            )
+        lib = _capi.bind(C.CDLL(LIB, mode=C.RTLD_LOCAL))
+        if lib.mz_abi_version() != 1 or lib.mz_backend() != b"hip-gfx950":
+            raise RuntimeError(f"{LIB} is not the hip-gfx950 backend of ABI 1")
+        _lib = lib
+        return lib

@@ -1,0 +1,68 @@
+"""Build the product HIP library in-tree: mazero_amd/_build/libmzmcts.so (gfx950).
+
+    python -m mazero_amd.build          # or __graft_entry__.build()
+
+Flags that matter for parity with the reference CPU tree (SURVEY.md §7 hard part 3):
+  -ffp-contract=off                          no FMA contraction of `a*b + c` (the reference's x86-64
+                                             -O2 build has no FMA instructions)
+  -fhip-fp32-correctly-rounded-divide-sqrt   IEEE f32 division (value = ws/tw, normalisation)
+  no -ffast-math, no denormal flushing
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "mzmcts.hip")
+OUT_DIR = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT_DIR, "libmzmcts.so")
+ARCH = os.environ.get("MZ_OFFLOAD_ARCH", "gfx950")
+
+FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-shared",
+    "-ffp-contract=off",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-fast-math",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X library cannot be built")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [SRC, os.path.join(ROOT, "include", "mzmcts.h"), __file__]
+    return any(os.path.getmtime(p) > t for p in deps)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), *FLAGS, "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp]
+    if verbose:
+        print("[mazero_amd] " + " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,1406 @@
+// mzmcts.hip — MI355X (gfx950) batched sampled-MCTS tree: HIP kernels + the C-ABI of
+// include/mzmcts.h.  Replaces the reference's CPU tree core (core/mcts/ctree/ctree_sampled/lib/
+// cnode.{h,cpp}, common_lib/utils.{h,cpp}) behind the same Tree_batch surface.
+//
+// Execution model.  One wavefront owns one tree for the whole kernel (grid = #trees, block = 64):
+// no cross-tree interaction exists in the algorithm (cnode.cpp:633-641, 663-669), so there is no
+// inter-workgroup communication at all.  Each launch stages the tree's hot node records from HBM
+// into LDS with LDS-DMA (global_load_lds), walks / updates the tree in LDS, and writes back only
+// the records it changed.  Per-simulation work is one launch (mz_expand_backup_select) fusing
+// expansion + back-propagation of simulation s with the selection of s+1 and the leaf
+// hidden-state gather that feeds the network.
+//
+// Data layout in HBM (tree-major structure of arrays; node n of tree t at index t*P + n, where
+// P = K*(S+2) is the reference's per-root pool, cnode.cpp:562):
+//   A[t][n]  int4  {visit, prior, val, reward}           read for every scored child
+//   Bn[t][n] int4  {first_child, nc | action<<16, pred_value, hidden_state_index_x}
+//   C[t][n]  float4{weighted_sum, tot_weight, -, -}       SubTreeValueSet scalars (utils.h:29)
+//   D[t][n]  float4{pred_prob, beta, beta_hat, -}         readback-only
+//   Q[t][n]  float  q = qsa - parent.pred_value           member of the min/max set (cnode.cpp:435,445)
+//   V[t][n][E] int2 {depth, value}                        every backed-up value of the node, sorted by
+//                                                         (depth, value); E = S+1 = max visits
+//   R[t][W]  u32   the tree's pre-generated std::mt19937 stream (cnode.cpp:574)
+// Children of a node are contiguous (the reference allocates them consecutively, cnode.cpp:290-292),
+// so scoring a node's children is one coalesced 16-B-per-lane LDS read.
+//
+// Bit-exactness.  Built with -ffp-contract=off, correctly rounded f32 division and no fast-math;
+// every float expression keeps the reference's operation order.  The pUCT log term uses a table
+// computed on the host with glibc logf (the reference calls logf, cnode.cpp:313), and sqrt(n) is
+// tabulated in double on the host too, so no device transcendental enters a result.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mzmcts.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kRngWin = 256;     // RNG words staged in LDS per launch
+constexpr int kMaxActions = 64;  // one lane per action
+constexpr int kMtN = 624;
+
+enum : int {
+    kErrPool = 1,      // node pool exhausted (more expansions than simulation_num allows)
+    kErrRng = 2,       // pre-generated RNG stream exhausted
+    kErrValueSet = 4,  // SubTreeValueSet::update invariant (utils.cpp:130)
+    kErrPath = 8,      // search path longer than the pool allows
+    kErrRoot = 16,     // selection on an unexpanded root (reference: UB, cnode.cpp:410)
+    kErrTable = 32,    // visit count beyond the pUCT table
+};
+
+struct TreeHdr {
+    int cursor, tot, D, err;
+    float mm_min, mm_max;
+    int mm_cnt, leaf;
+};
+
+struct Geo {
+    int B, A, K, S, P, E, W, PS;
+    int root_offset;
+    unsigned seed;
+    float one_minus_rho, delta;
+    int reg_cap;  // value entries staged in LDS per back-propagation chunk
+    // dynamic-LDS byte offsets of k_step
+    int oA, oB, oQ, oC, oPath, oPb, oSq, oLp, oRng, oBoot, oReg, lds;
+};
+
+struct Dev {
+    int4 *A;
+    int4 *Bn;
+    float4 *C;
+    float4 *D;
+    float *Q;
+    int2 *V;
+    unsigned *R;
+    TreeHdr *hdr;
+    int2 *path;  // [B][PS] {node, visit-at-selection}
+    long long *stats;
+    int *err;
+    float *pb;   // [PS] logf((n + c2 + 1)/c2) + c1
+    double *sq;  // [PS] sqrt(n)
+    float *lp;   // [PS+1] lambda^d as a float chain
+};
+
+struct StepArgs {
+    int hsx;
+    float discount;
+    int K;
+    const float *reward, *value, *policy, *beta;  // expansion inputs
+    float c2, c1;                                  // unused in-kernel (tables); kept for clarity
+    int *idx_x, *idy, *act;
+    const char *pool;
+    long long pool_stride, row_bytes;
+    char *gather_out;
+};
+
+struct PrepArgs {
+    const float *reward, *value, *policy, *beta, *noise;
+    float eps;
+    int K;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rlf(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double rld(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ float i2f(int x) { return __int_as_float(x); }
+__device__ __forceinline__ int f2i(float x) { return __float_as_int(x); }
+
+// Wait for this wave's LDS traffic (LDS-DMA included via vmcnt) and fence the compiler.
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// LDS-DMA: lane l copies `bytes` (4 or 16) from its own src into lds_base + l*bytes.
+__device__ __forceinline__ void glds4(const void *src, void *lds_base) {
+    __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)lds_base, 4, 0, 0);
+}
+__device__ __forceinline__ void glds16(const void *src, void *lds_base) {
+    __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int l = lane_id();
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int u = __shfl_up(v, o, kWave);
+        if (l >= o) v += u;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+
+// size_lim of SubTreeValueSet::update (utils.cpp:31): max(1, (int)ceil(count * (1 - rho)))
+__device__ __forceinline__ int value_lim(int c, float one_minus_rho) {
+    const int v = (int)ceilf((float)c * one_minus_rho);
+    return v < 1 ? 1 : v;
+}
+
+// --------------------------------------------------------------------------------------------
+// Stage: one tree's view of LDS
+// --------------------------------------------------------------------------------------------
+struct Lds {
+    int4 *A, *B;
+    float *Q;
+    float4 *C;
+    int2 *path;
+    float *pb;
+    double *sq;
+    float *lp;
+    unsigned *rng;
+    float *boot;
+    int2 *reg;
+    __device__ Lds(unsigned char *s, const Geo &g)
+        : A((int4 *)(s + g.oA)), B((int4 *)(s + g.oB)), Q((float *)(s + g.oQ)), C((float4 *)(s + g.oC)),
+          path((int2 *)(s + g.oPath)), pb((float *)(s + g.oPb)), sq((double *)(s + g.oSq)),
+          lp((float *)(s + g.oLp)), rng((unsigned *)(s + g.oRng)), boot((float *)(s + g.oBoot)),
+          reg((int2 *)(s + g.oReg)) {}
+};
+
+// RNG word `idx` of tree t: from the LDS window [wbase, wbase+kRngWin) or from HBM.
+__device__ __forceinline__ unsigned rng_word(const Geo &g, const Dev &d, const unsigned *win, int wbase, int t,
+                                             int idx, int &err) {
+    const int o = idx - wbase;
+    if (o >= 0 && o < kRngWin && win) return win[o];
+    if (idx >= g.W) {
+        err |= kErrRng;
+        return 0u;
+    }
+    return d.R[(size_t)t * g.W + idx];
+}
+
+// --------------------------------------------------------------------------------------------
+// CTree::expand (cnode.cpp:224-295) for one node, agent_num = 1.  Lane a < A holds the node's
+// policy / beta / noise entry for action a.  Children are created for the distinct sampled actions
+// in ascending order (std::map<long> key order, cnode.cpp:243,268).  Sampling restates
+// std::discrete_distribution<int> + generate_canonical<double,53> (libstdc++ random.tcc:
+// 2656-2713, 3348-3378): double prefix sums of beta/sum(beta), last forced to 1.0; two engine words
+// per draw; index = lower_bound.  Fewer than two actions => no draw and no engine word.
+// Returns nc; writes the children to HBM (and to the LDS mirrors when given).
+// --------------------------------------------------------------------------------------------
+__device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float bet, float noi, float eps, int K,
+                           int &cursor, int &tot, const unsigned *win, int wbase, int4 *sA, int4 *sB, float *sQ,
+                           int &err, long long &st_new) {
+    const int l = lane_id();
+    const int A = g.A;
+    int cnt = 0;  // number of draws that hit action l
+    if (A < 2) {
+        cnt = (l == 0) ? K : 0;
+    } else {
+        // cumulative distribution (param_type::_M_initialize)
+        const double bd = (l < A) ? (double)bet : 0.0;
+        double sum = 0.0;
+        for (int a = 0; a < A; ++a) sum += rld(bd, a);
+        const double p = bd / sum;
+        double acc = 0.0, cp = 0.0;
+        for (int a = 0; a < A; ++a) {
+            const double pa = rld(p, a);
+            acc = (a == 0) ? pa : acc + pa;
+            if (l == a) cp = acc;
+        }
+        if (l == A - 1) cp = 1.0;
+        // K draws, 64 at a time; lane k of a chunk performs draw k0+k
+        for (int k0 = 0; k0 < K; k0 += kWave) {
+            const int nk = (K - k0) < kWave ? (K - k0) : kWave;
+            int idx = 0;
+            if (l < nk) {
+                const int w = cursor + 2 * (k0 + l);
+                const double w1 = (double)rng_word(g, d, win, wbase, t, w, err);
+                const double w2 = (double)rng_word(g, d, win, wbase, t, w + 1, err);
+                double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
+                if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+                for (int a = 0; a < A; ++a) idx += (rld(cp, a) < u) ? 1 : 0;
+            }
+            for (int k = 0; k < nk; ++k) cnt += (rl(idx, k) == l) ? 1 : 0;
+        }
+        cursor += 2 * K;
+    }
+    const bool has = (l < A) && cnt > 0;
+    const unsigned long long m = ballot(has);
+    const int nc = __popcll(m);
+    if (tot + nc > g.P) {
+        err |= kErrPool;
+        return 0;
+    }
+    if (has) {
+        const int rank = __popcll(m & ((1ull << l) - 1ull));
+        const int c = tot + rank;
+        const float bh = (float)cnt / (float)K;              // betahat_prob = count / sampled_times
+        float prior = (eps > 0) ? (pol * (1 - eps) + noi * eps) : pol;
+        prior = prior * bh / bet;                             // prior * betahat_prob / beta_prob
+        const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+        const int4 b4 = make_int4(0, (l << 16), f2i(0.0f), -1);
+        const size_t gi = (size_t)t * g.P + c;
+        d.A[gi] = a4;
+        d.Bn[gi] = b4;
+        d.C[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d.D[gi] = make_float4(pol, bet, bh, 0.f);
+        d.Q[gi] = 0.f;
+        if (sA) {
+            sA[c] = a4;
+            sB[c] = b4;
+            sQ[c] = 0.f;
+        }
+    }
+    st_new += nc;
+    tot += nc;  // the children occupy [old tot, old tot + nc)
+    return nc;
+}
+
+// --------------------------------------------------------------------------------------------
+// Prepare (CTree_batch::prepare, cnode.cpp:589-614 -> CTree::prepare, cnode.cpp:205-222):
+// generate the tree's mt19937 stream (seed random_seed*2333 + i, cnode.cpp:574) with all four
+// waves, then expand the root with wave 0.
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned mt_twist(unsigned cur, unsigned nxt) {
+    const unsigned y = (cur & 0x80000000u) | (nxt & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ unsigned mt_temper(unsigned z) {
+    z ^= (z >> 11);
+    z ^= (z << 7) & 0x9d2c5680u;
+    z ^= (z << 15) & 0xefc60000u;
+    z ^= (z >> 18);
+    return z;
+}
+
+__global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
+    __shared__ unsigned mt[kMtN];
+    __shared__ unsigned w0[kMtN];
+    const int t = blockIdx.x;
+    const int tid = threadIdx.x;
+    if (tid == 0) {  // std::mt19937::seed: sequential by definition
+        unsigned x = g.seed * 2333u + (unsigned)(g.root_offset + t);
+        mt[0] = x;
+        for (int i = 1; i < kMtN; ++i) {
+            x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
+            mt[i] = x;
+        }
+    }
+    __syncthreads();
+    const int nb = g.W / kMtN;
+    for (int blk = 0; blk < nb; ++blk) {
+        unsigned v = 0;
+        // k in [0, 227): x[k] = x[k+397] ^ twist(x[k], x[k+1])       (all old)
+        if (tid < 227) v = mt[tid + 397] ^ mt_twist(mt[tid], mt[tid + 1]);
+        __syncthreads();
+        if (tid < 227) mt[tid] = v;
+        __syncthreads();
+        // k in [227, 454): x[k] = x[k-227](new) ^ twist(x[k], x[k+1])(old)
+        {
+            const int k = 227 + tid;
+            if (k < 454) v = mt[k - 227] ^ mt_twist(mt[k], mt[k + 1]);
+            __syncthreads();
+            if (k < 454) mt[k] = v;
+            __syncthreads();
+        }
+        // k in [454, 624): x[k] = x[k-227](new) ^ twist(x[k], x[k+1 or 0(new)])
+        {
+            const int k = 454 + tid;
+            if (k < kMtN) v = mt[k - 227] ^ mt_twist(mt[k], (k == kMtN - 1) ? mt[0] : mt[k + 1]);
+            __syncthreads();
+            if (k < kMtN) mt[k] = v;
+            __syncthreads();
+        }
+        unsigned *dst = d.R + (size_t)t * g.W + (size_t)blk * kMtN;
+        for (int k = tid; k < kMtN; k += blockDim.x) {
+            const unsigned z = mt_temper(mt[k]);
+            dst[k] = z;
+            if (blk == 0) w0[k] = z;
+        }
+        __syncthreads();
+    }
+    if (tid >= kWave) return;
+
+    // ---- root expansion by wave 0 ----
+    const int l = tid;
+    const int A = g.A;
+    const size_t ib = (size_t)t * A;
+    const float pol = (l < A) ? a.policy[ib + l] : 0.f;
+    const float bet = (l < A) ? a.beta[ib + l] : 0.f;
+    const float noi = (l < A) ? a.noise[ib + l] : 0.f;
+    const float r = a.reward[t];
+    const float v = a.value[t];
+    int err = 0;
+    int cursor = 0, tot = 1;
+    long long st_new = 0;
+    const int nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, cursor, tot, w0, 0, nullptr, nullptr, nullptr, err,
+                               st_new);
+    if (l == 0) {
+        // root: CNode(1,1,1,1,true) (cnode.cpp:217), expanded, visit += 1, subtree.update(value, 0)
+        const size_t gi = (size_t)t * g.P;
+        // first SubTreeValueSet::update: count 1, big and small empty -> insert into big
+        float ws = 0.f, tw = 0.f;
+        const float lp0 = d.lp[0];
+        if (value_lim(1, g.one_minus_rho) != 1) err |= kErrValueSet;
+        tw += lp0;
+        ws += lp0 * v;
+        const float val = (nc > 0) ? ws / tw : 0.f;
+        d.A[gi] = make_int4(1, f2i(1.0f), f2i(val), f2i(r));
+        d.Bn[gi] = make_int4(1, nc | (0 << 16), f2i(v), 0);
+        d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
+        d.D[gi] = make_float4(1.f, 1.f, 1.f, 0.f);
+        d.Q[gi] = 0.f;
+        d.V[gi * g.E] = make_int2(0, f2i(v));
+        TreeHdr h;
+        h.cursor = cursor;
+        h.tot = tot;
+        h.D = 0;
+        h.err = err;
+        h.mm_min = 0.f;
+        h.mm_max = 0.f;
+        h.mm_cnt = 0;
+        h.leaf = 0;
+        d.hdr[t] = h;
+        d.path[(size_t)t * g.PS] = make_int2(0, 1);
+        long long *st = d.stats + (size_t)t * MZ_S_COUNT;
+        st[MZ_S_EXPANDS] += 1;
+        st[MZ_S_NEW_CHILDREN] += st_new;
+        if (err) atomicOr(d.err, err);
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// CTree::back_propagate (cnode.cpp:415-450) over the path held in LDS.  Lane i owns path node i
+// (chunks of <= 64 nodes whose value entries fit the LDS staging area).  Bootstrap values are a
+// sequential f32 recurrence b_{i-1} = reward_i + discount * b_i, computed once by the whole wave.
+// Each node's SubTreeValueSet::update (utils.cpp:20-71) reads min(big) / max(small) as order
+// statistics of its sorted entries at that depth and replays the reference's f32 op sequence.
+// Afterwards the min/max normaliser (CMinMaxStats, utils.cpp:79-103) is recomputed as a reduction
+// over the q of every visited non-root node -- exactly the multiset's content.
+// --------------------------------------------------------------------------------------------
+__device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float disc, TreeHdr &h,
+                       int &err, long long *stl) {
+    const int l = lane_id();
+    // bootstrap values (cnode.cpp:424,448)
+    {
+        float b = value;
+        if (l == 0) s.boot[D] = b;
+        for (int base = D; base >= 1; base -= kWave) {
+            const int i = base - l;
+            const float r = (i >= 1) ? i2f(s.A[s.path[i].x].w) : 0.f;
+            const int n = base < kWave ? base : kWave;
+            float mine = 0.f;
+            for (int k = 0; k < n; ++k) {
+                const float rk = rlf(r, k);
+                b = rk + disc * b;
+                if (l == k) mine = b;
+            }
+            if (l < n) s.boot[base - l - 1] = mine;
+        }
+        wait_lds();
+    }
+    int2 *gV = d.V + (size_t)t * g.P * g.E;
+    for (int i0 = 0; i0 <= D;) {
+        const int i = i0 + l;
+        const bool act = i <= D;
+        const int2 pe = act ? s.path[i] : make_int2(0, 0);
+        const int n = pe.x, nv = pe.y;
+        const int inc = wave_incl_scan(act ? nv : 0);
+        const unsigned long long fm = ballot(act && inc <= g.reg_cap);
+        const int cnt = __popcll(fm);
+        if (cnt == 0) {
+            err |= kErrPath;
+            return;
+        }
+        const int off = inc - nv;
+        // stage the chunk's value entries with LDS-DMA (2 dwords per entry)
+        int *regdw = (int *)s.reg;
+        for (int j = 0; j < cnt; ++j) {
+            const int nj = rl(n, j), vj = rl(nv, j), oj = rl(off, j);
+            const int dw = 2 * vj;
+            const int *src = (const int *)(gV + (size_t)nj * g.E);
+            for (int c = 0; c < dw; c += kWave)
+                if (c + l < dw) glds4(src + c + l, regdw + 2 * oj + c);
+        }
+        wait_vm();
+        if (l < cnt) {
+            const int dep = D - i;
+            const float key = s.boot[i];
+            const int2 *R = s.reg + off;
+            int lo = 0, c = 0, pv = 0;
+            for (int j = 0; j < nv; ++j) {
+                const int2 e = R[j];
+                lo += (e.x < dep) ? 1 : 0;
+                const bool eq = (e.x == dep);
+                c += eq ? 1 : 0;
+                pv += (eq && i2f(e.y) < key) ? 1 : 0;
+            }
+            float4 cw = s.C[i];
+            float ws = cw.x, tw = cw.y;
+            const float lp = s.lp[dep];
+            const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
+            const int nl = value_lim(c + 1, g.one_minus_rho);
+            if (cur == nl) {
+                const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
+                if (!(key < mb)) {
+                    ws -= lp * mb;
+                    tw -= lp;
+                    tw += lp;
+                    ws += lp * key;
+                }
+            } else {
+                if (cur + 1 != nl) err |= kErrValueSet;
+                if (c - cur == 0) {
+                    tw += lp;
+                    ws += lp * key;
+                } else {
+                    const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
+                    if (key > ms) {
+                        tw += lp;
+                        ws += lp * key;
+                    } else {
+                        tw += lp;
+                        ws += lp * ms;
+                    }
+                }
+            }
+            // insert (dep, key) at its sorted place: shift the tail up by one in HBM
+            const int pos = lo + pv;
+            int2 *G = gV + (size_t)n * g.E;
+            if (nv + 1 > g.E) err |= kErrPath;
+            else {
+                for (int j = nv - 1; j >= pos; --j) G[j + 1] = R[j];
+                G[pos] = make_int2(dep, f2i(key));
+            }
+            stl[MZ_S_ENTRIES_READ] += nv;
+            stl[MZ_S_ENTRIES_WRITTEN] += nv - pos + 1;
+            // node scalars
+            const int4 a4 = s.A[n];
+            const int nc = s.B[n].y & 0xffff;
+            const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
+            const int4 na = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
+            s.A[n] = na;
+            const size_t gi = (size_t)t * g.P + n;
+            d.A[gi] = na;
+            d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
+            if (i >= 1) {
+                const float ppv = i2f(s.B[s.path[i - 1].x].z);
+                const float q = (i2f(a4.w) + disc * val) - ppv;  // get_qsa - father->pred_value
+                s.Q[n] = q;
+                d.Q[gi] = q;
+            }
+        }
+        wait_lds();
+        i0 += cnt;
+    }
+    stl[MZ_S_BACKUP_NODES] += D + 1;
+    // min/max over the q of visited non-root nodes
+    float mn = INFINITY, mx = -INFINITY;
+    int cv = 0;
+    for (int n = 1 + l; n < tot; n += kWave) {
+        if (s.A[n].x > 0) {
+            const float q = s.Q[n];
+            mn = fminf(mn, q);
+            mx = fmaxf(mx, q);
+            ++cv;
+        }
+    }
+    h.mm_min = wave_min(mn);
+    h.mm_max = wave_max(mx);
+    h.mm_cnt = wave_sum(cv);
+    stl[MZ_S_MINMAX_NODES] += tot - 1;
+}
+
+// --------------------------------------------------------------------------------------------
+// CTree::select_path (cnode.cpp:381-413) with select_child (337-379) and ucb_score (297-335),
+// walking the LDS copy.  Lane j scores child j; the arg-max with epsilon ties is the reference's
+// sequential scan over the lanes (uniform loop), one engine word when the tie list is non-empty.
+// --------------------------------------------------------------------------------------------
+__device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float disc, TreeHdr &h, int wbase, int &err,
+                            int &out_idx, int &out_act, long long *stl) {
+    const int l = lane_id();
+    int x = 0;
+    int4 xa = s.A[0];
+    int4 xb = s.B[0];
+    int4 pb_ = xb;  // parent's B (for hidden_state_index_x)
+    int D = 0;
+    if (l == 0) s.path[0] = make_int2(0, xa.x);
+    const bool mm_on = h.mm_cnt > 0;
+    const float mmn = h.mm_min, mmx = h.mm_max;
+    float den = 0.f;
+    if (mm_on) {
+        const float delta = mmx - mmn;
+        den = (g.delta < delta) ? delta : g.delta;  // std::max(delta_lb, delta)
+    }
+    long long scored = 0;
+    while (true) {
+        const int nc = xb.y & 0xffff;
+        if (nc == 0) break;
+        const int fc = xb.x;
+        // every lane reads its child's records (one LDS round trip per level)
+        const bool has = l < nc;
+        const int4 ca = has ? s.A[fc + l] : make_int4(0, 0, 0, 0);
+        const int4 cb = has ? s.B[fc + l] : make_int4(0, 0, 0, 0);
+        int ci;
+        if (x == 0 && xa.x <= nc) {
+            ci = xa.x - 1;  // forced root round-robin (cnode.cpp:398-399)
+        } else {
+            const int ntot = xa.x - 1;  // total_children_visit_counts = node->visit_count - 1
+            if (ntot < 0 || ntot >= g.PS) {
+                err |= kErrTable;
+                break;
+            }
+            const float pbl = s.pb[ntot];
+            const double sqn = s.sq[ntot];
+            float score = 0.f;
+            if (has) {
+                const int v = ca.x;
+                float pbc = pbl;
+                pbc = (float)((double)pbc * (sqn / (double)(v + 1)));
+                const float prior_score = pbc * i2f(ca.y);
+                float vs = (v == 0) ? 0.0f : ((i2f(ca.w) + disc * i2f(ca.z)) - i2f(xb.z));
+                if (mm_on) vs = (vs - mmn) / den;
+                if (vs < 0) vs = 0;
+                if (vs > 1) vs = 1;
+                score = prior_score + vs;
+            }
+            scored += nc;
+            float maxs = -1000000.0f;  // FLOAT_MIN (utils.h:12)
+            unsigned long long lst = 0ull;
+            for (int j = 0; j < nc; ++j) {
+                const float sj = rlf(score, j);
+                if (maxs < sj) {
+                    maxs = sj;
+                    lst = 1ull << j;
+                } else if (sj >= maxs - 0.000001f) {
+                    lst |= 1ull << j;
+                }
+            }
+            ci = 0;
+            const int cnt = __popcll(lst);
+            if (cnt > 0) {
+                const unsigned w = rng_word(g, d, s.rng, wbase, t, h.cursor, err);
+                h.cursor += 1;
+                int k = (int)(w % (unsigned)cnt);
+                for (; k > 0; --k) lst &= lst - 1ull;
+                ci = __builtin_ctzll(lst);
+            }
+        }
+        // descend
+        pb_ = xb;
+        x = fc + ci;
+        xa = make_int4(rl(ca.x, ci), rl(ca.y, ci), rl(ca.z, ci), rl(ca.w, ci));
+        xb = make_int4(rl(cb.x, ci), rl(cb.y, ci), rl(cb.z, ci), rl(cb.w, ci));
+        if (D + 1 >= g.PS) {
+            err |= kErrPath;
+            break;
+        }
+        ++D;
+        if (l == 0) s.path[D] = make_int2(x, xa.x);
+    }
+    if (D == 0) err |= kErrRoot;
+    h.D = D;
+    h.leaf = x;
+    out_idx = pb_.w;       // parent->hidden_state_index_x
+    out_act = xb.y >> 16;  // children_action of the last edge
+    stl[MZ_S_SELECTS] += 1;
+    stl[MZ_S_PATH_EDGES] += D;
+    stl[MZ_S_SCORED] += scored;
+    wait_lds();
+    // publish the path {node, visit} for the next back-propagation
+    int2 *gp = d.path + (size_t)t * g.PS;
+    for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
+}
+
+// --------------------------------------------------------------------------------------------
+// One simulation step of one tree: [expand + back-propagate (sim s)] -> [select (sim s+1)] ->
+// [gather the selected leaf's parent hidden state].
+// --------------------------------------------------------------------------------------------
+template <bool EB, bool SEL>
+__global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    Lds s(smem, g);
+    const int t = blockIdx.x;
+    const int l = threadIdx.x;
+    TreeHdr h = d.hdr[t];
+    if (h.err) {
+        if (SEL && l == 0) {
+            a.idx_x[t] = 0;
+            a.idy[t] = t;
+            a.act[t] = 0;
+        }
+        return;
+    }
+    int err = 0;
+    long long stl[MZ_S_COUNT];
+#pragma unroll
+    for (int k = 0; k < MZ_S_COUNT; ++k) stl[k] = 0;
+
+    // ---- round 1: tables, path, expansion inputs ----
+    // (LDS-DMA: lane l's element goes to base + 4*l, the base being uniform across the wave)
+    if (SEL) {
+        for (int i = l; i < g.PS; i += kWave) glds4(d.pb + i, s.pb + (i - l));
+        for (int i = l; i < 2 * g.PS; i += kWave) glds4((const int *)d.sq + i, (int *)s.sq + (i - l));
+    }
+    float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
+    if (EB) {
+        for (int i = l; i < g.PS + 1; i += kWave) glds4(d.lp + i, s.lp + (i - l));
+        for (int i = l; i < 2 * (h.D + 1); i += kWave)
+            glds4((const int *)(d.path + (size_t)t * g.PS) + i, (int *)s.path + (i - l));
+        const size_t ib = (size_t)t * g.A;
+        if (l < g.A) {
+            pol = a.policy[ib + l];
+            bet = a.beta[ib + l];
+        }
+        r_in = a.reward[t];
+        v_in = a.value[t];
+    }
+    wait_vm();
+
+    // ---- round 2: node records, q, path-node value scalars, RNG window ----
+    const int tot = h.tot;
+    const size_t nb = (size_t)t * g.P;
+    for (int i = l; i < ((tot + kWave - 1) / kWave) * kWave; i += kWave) {
+        if (i < tot) {
+            glds16(d.A + nb + i, s.A + (i - l));
+            glds16(d.Bn + nb + i, s.B + (i - l));
+            if (EB) glds4(d.Q + nb + i, s.Q + (i - l));
+        }
+    }
+    if (EB)
+        for (int i = l; i <= h.D; i += kWave) glds16(d.C + nb + s.path[i].x, s.C + (i - l));
+    const int wbase = h.cursor;
+    for (int i = l; i < kRngWin; i += kWave)
+        if (wbase + i < g.W) glds4(d.R + (size_t)t * g.W + wbase + i, s.rng + (i - l));
+    wait_vm();
+
+    int cursor = h.cursor;
+    int ntot = tot;
+    if (EB) {
+        // ---- CTree::expand_and_backprop (cnode.cpp:452-469) ----
+        const int leaf = s.path[h.D].x;
+        long long st_new = 0;
+        const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, cursor, ntot, s.rng, wbase, s.A, s.B, s.Q, err,
+                                   st_new);
+        stl[MZ_S_EXPANDS] += 1;
+        stl[MZ_S_NEW_CHILDREN] += st_new;
+        if (!err && l == 0) {
+            const int4 la = s.A[leaf];
+            const int4 lb = s.B[leaf];
+            const int4 na = make_int4(la.x, la.y, la.z, f2i(r_in));
+            const int4 nbv = make_int4(tot, nc | (lb.y & 0xffff0000), f2i(v_in), a.hsx);
+            s.A[leaf] = na;
+            s.B[leaf] = nbv;
+            d.A[nb + leaf] = na;
+            d.Bn[nb + leaf] = nbv;
+        }
+        wait_lds();
+        if (!err) {
+            h.cursor = cursor;
+            h.tot = ntot;
+            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, err, stl);
+        }
+    }
+    if (SEL && !err) {
+        int idx = 0, act = 0;
+        select_walk(g, d, s, t, a.discount, h, wbase, err, idx, act, stl);
+        if (l == 0) {
+            a.idx_x[t] = idx;
+            a.idy[t] = t;
+            a.act[t] = act;
+        }
+        if (a.pool) {  // mcts_sampled.py:130-134: leaf hidden state = pool[idx_x][t]
+            const char *src = a.pool + (long long)idx * a.pool_stride + (long long)t * a.row_bytes;
+            char *dst = a.gather_out + (long long)t * a.row_bytes;
+            const long long rb = a.row_bytes;
+            if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0) {
+                for (long long o = (long long)l * 16; o < rb; o += 16 * kWave)
+                    *(int4 *)(dst + o) = *(const int4 *)(src + o);
+            } else {
+                for (long long o = (long long)l * 4; o < rb; o += 4 * kWave) *(int *)(dst + o) = *(const int *)(src + o);
+            }
+        }
+    } else if (SEL && l == 0) {
+        a.idx_x[t] = 0;
+        a.idy[t] = t;
+        a.act[t] = 0;
+    }
+    if (l == 0) {
+        h.err = err;
+        d.hdr[t] = h;
+        long long *st = d.stats + (size_t)t * MZ_S_COUNT;
+#pragma unroll
+        for (int k = 0; k < MZ_S_COUNT; ++k) st[k] += stl[k];
+        if (err) atomicOr(d.err, err);
+    }
+}
+
+// Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
+__global__ __launch_bounds__(64) void k_gather(const char *pool, long long stride, long long rb, const int *idx,
+                                              char *out) {
+    const int t = blockIdx.x;
+    const int l = threadIdx.x;
+    const char *src = pool + (long long)idx[t] * stride + (long long)t * rb;
+    char *dst = out + (long long)t * rb;
+    if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0) {
+        for (long long o = (long long)l * 16; o < rb; o += 16 * kWave) *(int4 *)(dst + o) = *(const int4 *)(src + o);
+    } else {
+        for (long long o = (long long)l * 4; o < rb; o += 4 * kWave) *(int *)(dst + o) = *(const int *)(src + o);
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// Readbacks (cnode.cpp:672-781 over CNode getters 69-171), all fields in one pass.  Packed
+// field-major output (4-byte words):
+//   [B] root value | [B*A] marginal visits | [B*A] marginal priors | [B] degree |
+//   MZ_F_COUNT x [B*Wd] per-child fields padded with zeros to Wd = max degree
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int Wd, int *out) {
+    const int t = blockIdx.x;
+    const int l = threadIdx.x;
+    const int B = g.B, A = g.A;
+    const size_t nb = (size_t)t * g.P;
+    const int4 ra = d.A[nb];
+    const int4 rbn = d.Bn[nb];
+    const int nc = rbn.y & 0xffff;
+    const int fc = rbn.x;
+    float *fout = (float *)out;
+    if (l == 0) {
+        fout[t] = (nc > 0) ? i2f(ra.z) : 0.f;
+        out[B + 2 * B * A + t] = nc;
+    }
+    const bool has = l < nc;
+    int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
+    float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (has) {
+        ca = d.A[nb + fc + l];
+        cb = d.Bn[nb + fc + l];
+        cd = d.D[nb + fc + l];
+    }
+    const int act = cb.y >> 16;
+    // marginal visit counts / priors: lane a collects the child whose action is a
+    int mv = 0;
+    float mp = 0.f;
+    for (int j = 0; j < nc; ++j) {
+        const int aj = rl(act, j), vj = rl(ca.x, j);
+        const float pj = rlf(i2f(ca.y), j);
+        if (aj == l) {
+            mv += vj;
+            mp += pj;
+        }
+    }
+    if (l < A) {
+        out[B + (size_t)t * A + l] = mv;
+        fout[B + B * A + (size_t)t * A + l] = mp;
+    }
+    if (l < Wd) {
+        const size_t base = (size_t)2 * B + 2 * (size_t)B * A;
+        const size_t o = (size_t)t * Wd + l;
+        const size_t fs = (size_t)B * Wd;
+        const float val = i2f(ca.z);  // CNode::value(): 0 when not expanded (stored that way)
+        const float rew = i2f(ca.w);
+        out[base + MZ_F_ACTIONS * fs + o] = has ? act : 0;
+        out[base + MZ_F_VISIT_COUNT * fs + o] = has ? ca.x : 0;
+        fout[base + MZ_F_PRED_PROBS * fs + o] = has ? cd.x : 0.f;
+        fout[base + MZ_F_BETA * fs + o] = has ? cd.y : 0.f;
+        fout[base + MZ_F_BETA_HAT * fs + o] = has ? cd.z : 0.f;
+        fout[base + MZ_F_PRIORS * fs + o] = has ? i2f(ca.y) : 0.f;
+        fout[base + MZ_F_IMP_RATIO * fs + o] = has ? (cd.z / cd.y * cd.x) : 0.f;
+        fout[base + MZ_F_PRED_VALUES * fs + o] = has ? i2f(cb.z) : 0.f;
+        fout[base + MZ_F_MCTS_VALUES * fs + o] = has ? val : 0.f;
+        fout[base + MZ_F_REWARDS * fs + o] = has ? rew : 0.f;
+        fout[base + MZ_F_QVALUES * fs + o] = has ? (rew + disc * val) : 0.f;
+    }
+}
+
+}  // namespace
+
+// ================================================================================================
+// Host side
+// ================================================================================================
+struct mz_batch {
+    int B, N, A, K, S, P, E, W, PS, Wd;
+    int device;
+    Geo geo;
+    Dev dev;
+    hipStream_t stream = nullptr;
+    std::vector<void *> allocs;
+    float *in_dev = nullptr;  // host-input staging [B*(2+3A)]
+    int *sel_dev = nullptr;   // select output staging [3B]
+    int *rb_dev = nullptr;    // packed readback
+    size_t rb_words = 0;
+    std::vector<int> rb_host;
+    bool rb_valid = false;      // rb_host mirrors the current tree state
+    bool rb_dev_valid = false;  // rb_dev mirrors the current tree state
+    float rb_disc = 0.f;
+    float tbl_c2 = NAN, tbl_c1 = NAN;
+    bool prepared = false;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &m) {
+    g_err = m;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess) return fail(MZ_ERR_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+    } while (0)
+
+int round16(int x) { return (x + 15) & ~15; }
+
+const char *err_message(int bits) {
+    if (bits & kErrValueSet) return "SubTreeValueSet::update: cur_size+1!=size_lim.";
+    if (bits & kErrPool) return "node pool exhausted: more expansions than simulation_num allows";
+    if (bits & kErrRng) return "random stream exhausted: more simulations than simulation_num allows";
+    if (bits & kErrPath) return "search path or value-set capacity exceeded";
+    if (bits & kErrRoot) return "selection on an unexpanded root";
+    if (bits & kErrTable) return "visit count beyond the pUCT table (more simulations than simulation_num)";
+    return "device-side search error";
+}
+
+int ensure_device(mz_batch *b) {
+    int cur = -1;
+    HIP_TRY(hipGetDevice(&cur));
+    if (cur != b->device) HIP_TRY(hipSetDevice(b->device));
+    return MZ_OK;
+}
+
+// Poll the handle's error word (synchronises the stream).
+int check_device_errors(mz_batch *b) {
+    int e = 0;
+    HIP_TRY(hipMemcpyAsync(&e, b->dev.err, sizeof(int), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    if (e) return fail(MZ_ERR_RUNTIME, err_message(e));
+    return MZ_OK;
+}
+
+// pUCT tables for (c2, c1): pb[n] = logf(((float)n + c2 + 1) / c2) + c1 with glibc logf, exactly as
+// ucb_score evaluates it (cnode.cpp:313), and sq[n] = sqrt((double)n) (cnode.cpp:314).
+int ensure_tables(mz_batch *b, float c2, float c1) {
+    if (b->tbl_c2 == c2 && b->tbl_c1 == c1) return MZ_OK;
+    std::vector<float> pb(b->PS);
+    std::vector<double> sq(b->PS);
+    for (int n = 0; n < b->PS; ++n) {
+        float x = (float)n + c2;
+        x = x + 1.0f;
+        x = x / c2;
+        pb[n] = ::logf(x) + c1;
+        sq[n] = ::sqrt((double)n);
+    }
+    HIP_TRY(hipMemcpyAsync(b->dev.pb, pb.data(), sizeof(float) * b->PS, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->dev.sq, sq.data(), sizeof(double) * b->PS, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    b->tbl_c2 = c2;
+    b->tbl_c1 = c1;
+    return MZ_OK;
+}
+
+template <typename T>
+int dalloc(mz_batch *b, T **p, size_t count) {
+    void *q = nullptr;
+    HIP_TRY(hipMalloc(&q, count * sizeof(T) + 64));
+    b->allocs.push_back(q);
+    *p = (T *)q;
+    return MZ_OK;
+}
+
+int launch_step(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
+    const Geo &g = b->geo;
+    if (eb && sel)
+        hipLaunchKernelGGL((k_step<true, true>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
+    else if (eb)
+        hipLaunchKernelGGL((k_step<true, false>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
+    else
+        hipLaunchKernelGGL((k_step<false, true>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
+    HIP_TRY(hipGetLastError());
+    if (eb) b->rb_valid = b->rb_dev_valid = false;
+    return MZ_OK;
+}
+
+// Packed readback computed on the device (stream-ordered, no synchronisation).
+int readback_dev(mz_batch *b, float disc) {
+    if (b->rb_dev_valid && b->rb_disc == disc) return MZ_OK;
+    hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->geo, b->dev, disc, b->Wd, b->rb_dev);
+    HIP_TRY(hipGetLastError());
+    b->rb_dev_valid = true;
+    b->rb_valid = false;
+    b->rb_disc = disc;
+    return MZ_OK;
+}
+
+// ... and mirrored to the host (synchronises; reports deferred device errors).
+int readback(mz_batch *b, float disc) {
+    if (b->rb_valid && b->rb_disc == disc) return MZ_OK;
+    int rc = readback_dev(b, disc);
+    if (rc) return rc;
+    b->rb_host.resize(b->rb_words);
+    HIP_TRY(hipMemcpyAsync(b->rb_host.data(), b->rb_dev, sizeof(int) * b->rb_words, hipMemcpyDeviceToHost, b->stream));
+    rc = check_device_errors(b);
+    if (rc) return rc;
+    b->rb_valid = true;
+    return MZ_OK;
+}
+
+size_t rb_field_base(const mz_batch *b, int field) {
+    return (size_t)2 * b->B + 2 * (size_t)b->B * b->A + (size_t)field * b->B * b->Wd;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mz_last_error(void) { return g_err.c_str(); }
+int mz_abi_version(void) { return MZ_ABI_VERSION; }
+const char *mz_backend(void) { return "hip-gfx950"; }
+
+int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, float rho, float lam, int root_offset,
+              mz_batch **out) {
+    if (!out) return fail(MZ_ERR_ARG, "null output handle");
+    *out = nullptr;
+    if (B < 1 || A < 1 || K < 1 || S < 0) return fail(MZ_ERR_ARG, "bad tree-batch dimensions");
+    if (N != 1)
+        return fail(MZ_ERR_UNSUPPORTED,
+                    "agent_num != 1: the per-agent sequential search of this fork builds 1-agent trees "
+                    "(mcts_sampled.py:53,89); joint-action trees are not implemented on the GPU yet");
+    if (A > kMaxActions) return fail(MZ_ERR_UNSUPPORTED, "action_space_size > 64");
+    if (K > 4096) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 4096");
+    auto *b = new mz_batch;
+    b->B = B;
+    b->N = N;
+    b->A = A;
+    b->K = K;
+    b->S = S;
+    b->P = K * (S + 2);
+    b->E = S + 1;
+    b->PS = S + 2;
+    b->Wd = (K < A ? K : A);
+    if (b->Wd < 1) b->Wd = 1;
+    // RNG words a search can consume: 2K per expansion (S+1 of them, +1 slack) and at most
+    // (leaf depth) words per selection, sum_{s<=S} (s+1); rounded up to whole 624-word blocks.
+    {
+        const long long need = 2ll * K * (S + 2) + (long long)(S + 1) * (S + 2) / 2 + kRngWin;
+        b->W = (int)(((need + kMtN - 1) / kMtN) * kMtN);
+    }
+    if (hipGetDevice(&b->device) != hipSuccess) {
+        delete b;
+        return fail(MZ_ERR_DEVICE, "no HIP device");
+    }
+    Geo &g = b->geo;
+    g.B = B;
+    g.A = A;
+    g.K = K;
+    g.S = S;
+    g.P = b->P;
+    g.E = b->E;
+    g.W = b->W;
+    g.PS = b->PS;
+    g.root_offset = root_offset;
+    g.seed = seed;
+    g.one_minus_rho = 1 - rho;
+    g.delta = delta_lb;
+    {
+        // worst case of sum(visits) over a path: every value entry of the tree
+        const long long worst = 1ll + S + (long long)S * (S + 1) / 2;
+        long long cap = worst < 4096 ? worst : 4096;  // <= 32 KiB of staged entries per chunk
+        if (cap < S + 1) cap = S + 1;
+        g.reg_cap = (int)cap;
+    }
+    int o = 0;
+    g.oA = o; o += round16(16 * g.P);
+    g.oB = o; o += round16(16 * g.P);
+    g.oQ = o; o += round16(4 * g.P);
+    g.oC = o; o += round16(16 * g.PS);
+    g.oPath = o; o += round16(8 * g.PS);
+    g.oPb = o; o += round16(4 * (g.PS + kWave));
+    g.oSq = o; o += round16(8 * (g.PS + kWave));
+    g.oLp = o; o += round16(4 * (g.PS + 1 + kWave));
+    g.oRng = o; o += round16(4 * kRngWin);
+    g.oBoot = o; o += round16(4 * g.PS);
+    g.oReg = o; o += round16(8 * g.reg_cap);
+    g.lds = o;
+    if (g.lds > 160 * 1024) {
+        delete b;
+        return fail(MZ_ERR_UNSUPPORTED, "tree too large for the LDS-resident kernels (K*(S+2) nodes)");
+    }
+    Dev &d = b->dev;
+    const size_t nodes = (size_t)B * b->P;
+    int rc = 0;
+    rc |= dalloc(b, &d.A, nodes);
+    rc |= dalloc(b, &d.Bn, nodes);
+    rc |= dalloc(b, &d.C, nodes);
+    rc |= dalloc(b, &d.D, nodes);
+    rc |= dalloc(b, &d.Q, nodes);
+    rc |= dalloc(b, &d.V, nodes * b->E);
+    rc |= dalloc(b, &d.R, (size_t)B * b->W);
+    rc |= dalloc(b, &d.hdr, (size_t)B);
+    rc |= dalloc(b, &d.path, (size_t)B * b->PS);
+    rc |= dalloc(b, &d.stats, (size_t)B * MZ_S_COUNT);
+    rc |= dalloc(b, &d.err, 1);
+    rc |= dalloc(b, &d.pb, (size_t)b->PS + kWave);
+    rc |= dalloc(b, &d.sq, (size_t)b->PS + kWave);
+    rc |= dalloc(b, &d.lp, (size_t)b->PS + 1 + kWave);
+    rc |= dalloc(b, &b->in_dev, (size_t)B * (2 + 3 * A));
+    rc |= dalloc(b, &b->sel_dev, (size_t)3 * B);
+    b->rb_words = (size_t)2 * B + 2 * (size_t)B * A + (size_t)MZ_F_COUNT * B * b->Wd;
+    rc |= dalloc(b, &b->rb_dev, b->rb_words);
+    if (rc) {
+        std::string m = g_err;
+        mz_destroy(b);
+        return fail(MZ_ERR_DEVICE, m);
+    }
+    std::vector<float> lp(b->PS + 1 + kWave, 0.f);
+    lp[0] = 1.0f;
+    for (int k = 1; k < b->PS + 1; ++k) lp[k] = lp[k - 1] * lam;  // lam_pow chain (utils.cpp:25-27)
+    if (hipMemcpy(d.lp, lp.data(), sizeof(float) * lp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d.hdr, 0, sizeof(TreeHdr) * B) != hipSuccess ||
+        hipMemset(d.stats, 0, sizeof(long long) * B * MZ_S_COUNT) != hipSuccess ||
+        hipMemset(d.err, 0, sizeof(int)) != hipSuccess) {
+        mz_destroy(b);
+        return fail(MZ_ERR_DEVICE, "device initialisation failed");
+    }
+    if (g.lds > 64 * 1024) {
+        (void)hipFuncSetAttribute((const void *)k_step<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+        (void)hipFuncSetAttribute((const void *)k_step<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+        (void)hipFuncSetAttribute((const void *)k_step<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+    }
+    *out = b;
+    return MZ_OK;
+}
+
+int mz_destroy(mz_batch *b) {
+    if (!b) return MZ_OK;
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    else (void)hipDeviceSynchronize();
+    for (void *p : b->allocs) (void)hipFree(p);
+    delete b;
+    return MZ_OK;
+}
+
+int mz_set_stream(mz_batch *b, void *stream) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    b->stream = (hipStream_t)stream;
+    return MZ_OK;
+}
+
+int mz_synchronize(mz_batch *b) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    return check_device_errors(b);
+}
+
+int mz_prepare(mz_batch *b, const float *rewards, const float *values, const float *policy, const float *beta, int K,
+               float noise_eps, const float *noises, int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    const size_t B = b->B, NA = (size_t)b->A;
+    PrepArgs a;
+    if (mem == MZ_MEM_HOST) {
+        float *p = b->in_dev;
+        HIP_TRY(hipMemcpyAsync(p, rewards, 4 * B, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + B, values, 4 * B, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + 2 * B, policy, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + 2 * B + B * NA, beta, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + 2 * B + 2 * B * NA, noises, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
+        a.reward = p;
+        a.value = p + B;
+        a.policy = p + 2 * B;
+        a.beta = p + 2 * B + B * NA;
+        a.noise = p + 2 * B + 2 * B * NA;
+    } else if (mem == MZ_MEM_DEVICE) {
+        a.reward = rewards;
+        a.value = values;
+        a.policy = policy;
+        a.beta = beta;
+        a.noise = noises;
+    } else {
+        return fail(MZ_ERR_ARG, "bad memory kind");
+    }
+    a.eps = noise_eps;
+    a.K = K;
+    HIP_TRY(hipMemsetAsync(b->dev.err, 0, sizeof(int), b->stream));
+    hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), 0, b->stream, b->geo, b->dev, a);
+    HIP_TRY(hipGetLastError());
+    b->rb_valid = b->rb_dev_valid = false;
+    b->prepared = true;
+    if (mem == MZ_MEM_HOST) return check_device_errors(b);
+    return MZ_OK;
+}
+
+int mz_select(mz_batch *b, float c2, float c1, float discount, int32_t *idx_x, int32_t *idy, int32_t *actions,
+              int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (!b->prepared) return fail(MZ_ERR_RUNTIME, "batch_selection before prepare");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = ensure_tables(b, c2, c1);
+    if (rc) return rc;
+    StepArgs a{};
+    a.discount = discount;
+    a.c2 = c2;
+    a.c1 = c1;
+    if (mem == MZ_MEM_HOST) {
+        a.idx_x = b->sel_dev;
+        a.idy = b->sel_dev + b->B;
+        a.act = b->sel_dev + 2 * b->B;
+    } else if (mem == MZ_MEM_DEVICE) {
+        a.idx_x = idx_x;
+        a.idy = idy;
+        a.act = actions;
+    } else {
+        return fail(MZ_ERR_ARG, "bad memory kind");
+    }
+    rc = launch_step(b, false, true, a);
+    if (rc) return rc;
+    if (mem == MZ_MEM_HOST) {
+        std::vector<int32_t> tmp(3 * (size_t)b->B);
+        HIP_TRY(hipMemcpyAsync(tmp.data(), b->sel_dev, sizeof(int32_t) * tmp.size(), hipMemcpyDeviceToHost, b->stream));
+        rc = check_device_errors(b);
+        if (rc) return rc;
+        std::memcpy(idx_x, tmp.data(), sizeof(int32_t) * b->B);
+        std::memcpy(idy, tmp.data() + b->B, sizeof(int32_t) * b->B);
+        std::memcpy(actions, tmp.data() + 2 * b->B, sizeof(int32_t) * b->B);
+    }
+    return MZ_OK;
+}
+
+static int expand_inputs(mz_batch *b, const float *rewards, const float *values, const float *policy,
+                         const float *beta, int mem, StepArgs &a) {
+    const size_t B = b->B, NA = (size_t)b->A;
+    if (mem == MZ_MEM_HOST) {
+        float *p = b->in_dev;
+        HIP_TRY(hipMemcpyAsync(p, rewards, 4 * B, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + B, values, 4 * B, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + 2 * B, policy, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(p + 2 * B + B * NA, beta, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
+        a.reward = p;
+        a.value = p + B;
+        a.policy = p + 2 * B;
+        a.beta = p + 2 * B + B * NA;
+    } else if (mem == MZ_MEM_DEVICE) {
+        a.reward = rewards;
+        a.value = values;
+        a.policy = policy;
+        a.beta = beta;
+    } else {
+        return fail(MZ_ERR_ARG, "bad memory kind");
+    }
+    return MZ_OK;
+}
+
+int mz_expand_backup(mz_batch *b, int hsx, float discount, int K, const float *rewards, const float *values,
+                     const float *policy, const float *beta, int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (!b->prepared) return fail(MZ_ERR_RUNTIME, "batch_expansion_and_backup before prepare");
+    if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    StepArgs a{};
+    a.hsx = hsx;
+    a.discount = discount;
+    a.K = K;
+    rc = expand_inputs(b, rewards, values, policy, beta, mem, a);
+    if (rc) return rc;
+    rc = launch_step(b, true, false, a);
+    if (rc) return rc;
+    if (mem == MZ_MEM_HOST) return check_device_errors(b);
+    return MZ_OK;
+}
+
+int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const float *rewards, const float *values,
+                            const float *policy, const float *beta, float c2, float c1, int32_t *idx_x, int32_t *idy,
+                            int32_t *actions, const void *pool, int64_t pool_slot_stride, int64_t row_bytes,
+                            void *gather_out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (!b->prepared) return fail(MZ_ERR_RUNTIME, "expansion before prepare");
+    if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
+    if (pool && (!gather_out || row_bytes <= 0 || (row_bytes & 3)))
+        return fail(MZ_ERR_ARG, "gather needs an output buffer and row_bytes a positive multiple of 4");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = ensure_tables(b, c2, c1);
+    if (rc) return rc;
+    StepArgs a{};
+    a.hsx = hsx;
+    a.discount = discount;
+    a.K = K;
+    a.c2 = c2;
+    a.c1 = c1;
+    rc = expand_inputs(b, rewards, values, policy, beta, MZ_MEM_DEVICE, a);
+    if (rc) return rc;
+    a.idx_x = idx_x;
+    a.idy = idy;
+    a.act = actions;
+    a.pool = (const char *)pool;
+    a.pool_stride = pool_slot_stride;
+    a.row_bytes = row_bytes;
+    a.gather_out = (char *)gather_out;
+    return launch_step(b, true, true, a);
+}
+
+int mz_gather_rows(mz_batch *b, const void *pool, int64_t stride, int64_t row_bytes, const int32_t *idx_x, void *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (row_bytes <= 0 || (row_bytes & 3)) return fail(MZ_ERR_ARG, "row_bytes must be a positive multiple of 4");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_gather, dim3(b->B), dim3(kWave), 0, b->stream, (const char *)pool, (long long)stride,
+                       (long long)row_bytes, (const int *)idx_x, (char *)out);
+    HIP_TRY(hipGetLastError());
+    return MZ_OK;
+}
+
+int mz_get_roots_values(mz_batch *b, float *out, int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    if (mem == MZ_MEM_DEVICE) {
+        rc = readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(out, b->rb_dev, 4 * (size_t)b->B, hipMemcpyDeviceToDevice, b->stream));
+        return MZ_OK;
+    }
+    rc = readback(b, b->rb_valid ? b->rb_disc : 0.f);
+    if (rc) return rc;
+    std::memcpy(out, b->rb_host.data(), 4 * (size_t)b->B);
+    return MZ_OK;
+}
+
+int mz_get_roots_marginal_visit_count(mz_batch *b, int32_t *out, int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
+                                : readback(b, b->rb_valid ? b->rb_disc : 0.f);
+    if (rc) return rc;
+    const size_t n = (size_t)b->B * b->A;
+    if (mem == MZ_MEM_DEVICE) {
+        HIP_TRY(hipMemcpyAsync(out, b->rb_dev + b->B, 4 * n, hipMemcpyDeviceToDevice, b->stream));
+        return MZ_OK;
+    }
+    std::memcpy(out, b->rb_host.data() + b->B, 4 * n);
+    return MZ_OK;
+}
+
+int mz_get_roots_marginal_priors(mz_batch *b, float *out, int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
+                                : readback(b, b->rb_valid ? b->rb_disc : 0.f);
+    if (rc) return rc;
+    const size_t n = (size_t)b->B * b->A;
+    if (mem == MZ_MEM_DEVICE) {
+        HIP_TRY(hipMemcpyAsync(out, b->rb_dev + b->B + n, 4 * n, hipMemcpyDeviceToDevice, b->stream));
+        return MZ_OK;
+    }
+    std::memcpy(out, b->rb_host.data() + b->B + n, 4 * n);
+    return MZ_OK;
+}
+
+int mz_get_num_children_of_root(mz_batch *b, int tree_id, int32_t *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (tree_id < 0 || tree_id >= b->B) return fail(MZ_ERR_ARG, "tree_id out of range");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = readback(b, b->rb_valid ? b->rb_disc : 0.f);
+    if (rc) return rc;
+    *out = b->rb_host[(size_t)b->B + 2 * (size_t)b->B * b->A + tree_id];
+    return MZ_OK;
+}
+
+int mz_max_children(mz_batch *b, int32_t *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    *out = b->Wd;
+    return MZ_OK;
+}
+
+int mz_get_root_sampled(mz_batch *b, int field, int tree_id, float discount, void *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (tree_id < 0 || tree_id >= b->B) return fail(MZ_ERR_ARG, "tree_id out of range");
+    if (field < 0 || field >= MZ_F_COUNT) return fail(MZ_ERR_ARG, "unknown field");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = readback(b, field == MZ_F_QVALUES ? discount : (b->rb_valid ? b->rb_disc : discount));
+    if (rc) return rc;
+    const int deg = b->rb_host[(size_t)b->B + 2 * (size_t)b->B * b->A + tree_id];
+    std::memcpy(out, b->rb_host.data() + rb_field_base(b, field) + (size_t)tree_id * b->Wd, 4 * (size_t)deg);
+    return MZ_OK;
+}
+
+int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *out, int32_t *degrees, int mem) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (field < 0 || field >= MZ_F_COUNT) return fail(MZ_ERR_ARG, "unknown field");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    const float disc = field == MZ_F_QVALUES ? discount : ((b->rb_valid || b->rb_dev_valid) ? b->rb_disc : discount);
+    rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, disc) : readback(b, disc);
+    if (rc) return rc;
+    const size_t n = (size_t)b->B * b->Wd;
+    const size_t dego = (size_t)b->B + 2 * (size_t)b->B * b->A;
+    if (mem == MZ_MEM_DEVICE) {
+        HIP_TRY(hipMemcpyAsync(out, b->rb_dev + rb_field_base(b, field), 4 * n, hipMemcpyDeviceToDevice, b->stream));
+        if (degrees)
+            HIP_TRY(hipMemcpyAsync(degrees, b->rb_dev + dego, 4 * (size_t)b->B, hipMemcpyDeviceToDevice, b->stream));
+        return MZ_OK;
+    }
+    std::memcpy(out, b->rb_host.data() + rb_field_base(b, field), 4 * n);
+    if (degrees) std::memcpy(degrees, b->rb_host.data() + dego, 4 * (size_t)b->B);
+    return MZ_OK;
+}
+
+int mz_get_stats(mz_batch *b, int64_t *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    std::vector<long long> st((size_t)b->B * MZ_S_COUNT);
+    HIP_TRY(hipMemcpyAsync(st.data(), b->dev.stats, sizeof(long long) * st.size(), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    for (int k = 0; k < MZ_S_COUNT; ++k) out[k] = 0;
+    for (int t = 0; t < b->B; ++t)
+        for (int k = 0; k < MZ_S_COUNT; ++k) out[k] += st[(size_t)t * MZ_S_COUNT + k];
+    return MZ_OK;
+}
+
+int mz_print(mz_batch *b) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    std::vector<TreeHdr> h(b->B);
+    HIP_TRY(hipMemcpyAsync(h.data(), b->dev.hdr, sizeof(TreeHdr) * b->B, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    for (int t = 0; t < b->B; ++t)
+        fprintf(stderr, "tree %d: nodes %d, rng cursor %d, last path length %d, err %d, minmax [%f, %f] (%d)\n", t,
+                h[t].tot, h[t].cursor, h[t].D, h[t].err, h[t].mm_min, h[t].mm_max, h[t].mm_cnt);
+    return MZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,305 @@
+"""Drop-in replacement for the reference's Cython binding `cytree.Tree_batch`
+(core/mcts/ctree/ctree_sampled/cytree.pyx:7-247), backed by the C-ABI of include/mzmcts.h.
+
+Same constructor arguments, same methods, same return types (Python lists of int for the
+selection indices, numpy int32/float32 arrays for everything else, per-root lists for the
+`get_roots_sampled_*` readbacks).  Inputs follow cytree.pyx:22-47: any shape, reshaped to 1-D,
+made C-contiguous, and they must be float32 (Cython raises ValueError on a dtype mismatch, so
+does this class).
+
+Besides numpy arrays, every input may be a torch tensor already on the GPU: it is then passed
+zero-copy as a device pointer and the call is enqueued on the current torch stream instead of
+synchronising.  The `*_device` variants return torch tensors and never synchronise; they are what
+the device-resident driver (mazero_amd.mcts_sampled) uses.
+
+By default the product HIP library is used; `lib=` lets the tests drive an oracle library
+through this very class.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+from ._capi import FIELDS, INT_FIELDS, MZ_MEM_DEVICE, MZ_MEM_HOST, check
+
+try:  # torch is plumbing for device memory/streams; the host path works without it
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def _is_device_tensor(x) -> bool:
+    return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
+
+
+def _f32_host(x) -> np.ndarray:
+    if torch is not None and isinstance(x, torch.Tensor):
+        x = x.detach().cpu().numpy()
+    x = np.asarray(x).reshape(-1)
+    if x.dtype != np.float32:
+        raise ValueError(f"Buffer dtype mismatch, expected 'float' but got '{x.dtype}'")
+    if not x.flags["C_CONTIGUOUS"]:
+        x = np.ascontiguousarray(x)
+    return x
+
+
+def _f32_dev(x):
+    x = x.reshape(-1)
+    if x.dtype != torch.float32:
+        raise ValueError(f"Buffer dtype mismatch, expected 'float' but got '{x.dtype}'")
+    return x.contiguous()
+
+
+class Tree_batch:
+    """cytree.pyx:7 `cdef class Tree_batch` — one batch of independent sampled-MCTS trees."""
+
+    def __init__(
+        self,
+        root_num: int,
+        agent_num: int,
+        action_space_size: int,
+        sampled_times: int,
+        simulation_num: int,
+        tree_value_stat_delta_lb: float,
+        random_seed: int,
+        rho: float,
+        lam: float,
+        *,
+        root_offset: int = 0,
+        lib=None,
+    ):
+        if lib is None:
+            from ._lib import load
+
+            lib = load()
+        self._lib = lib
+        self.root_num = int(root_num)
+        self.agent_num = int(agent_num)
+        self.action_space_size = int(action_space_size)
+        self._h = C.c_void_p()
+        rc = lib.mz_create(
+            self.root_num,
+            self.agent_num,
+            self.action_space_size,
+            int(sampled_times),
+            int(simulation_num),
+            float(tree_value_stat_delta_lb),
+            int(random_seed) & 0xFFFFFFFF,
+            float(rho),
+            float(lam),
+            int(root_offset),
+            C.byref(self._h),
+        )
+        check(lib, rc, "Tree_batch")
+        self._keep = []  # host buffers that must outlive an enqueued call
+        self._stream_ptr = None
+        self._maxdeg = None
+
+    # -- lifetime ---------------------------------------------------------------------------
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self._lib.mz_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def _sync_stream(self):
+        """Bind the handle to torch's current stream (device path only)."""
+        if torch is None:
+            return
+        s = torch.cuda.current_stream().cuda_stream
+        if s != self._stream_ptr:
+            check(self._lib, self._lib.mz_set_stream(self._h, C.c_void_p(s)), "set_stream")
+            self._stream_ptr = s
+
+    def _inputs(self, *arrays):
+        """Returns (pointers, mem, keepalive)."""
+        dev = [_is_device_tensor(a) for a in arrays]
+        if any(dev):
+            if not all(dev):
+                raise ValueError("mix of host and device inputs")
+            ts = [_f32_dev(a) for a in arrays]
+            self._sync_stream()
+            return [C.c_void_p(t.data_ptr()) for t in ts], MZ_MEM_DEVICE, ts
+        hs = [_f32_host(a) for a in arrays]
+        return [h.ctypes.data_as(C.c_void_p) for h in hs], MZ_MEM_HOST, hs
+
+    # -- search (cytree.pyx:21-91) --------------------------------------------------------------
+    def prepare(self, rewards, values, policy_probs, beta, sampled_times, noise_eps, noises):
+        ptrs, mem, keep = self._inputs(rewards, values, policy_probs, beta, noises)
+        rc = self._lib.mz_prepare(
+            self._h, ptrs[0], ptrs[1], ptrs[2], ptrs[3], int(sampled_times), float(noise_eps), ptrs[4], mem
+        )
+        check(self._lib, rc, "prepare")
+        self._maxdeg = None
+
+    def batch_selection(self, pb_c_base, pb_c_init, discount):
+        B, N = self.root_num, self.agent_num
+        idx = np.empty(B, np.int32)
+        idy = np.empty(B, np.int32)
+        act = np.empty(B * N, np.int32)
+        rc = self._lib.mz_select(
+            self._h,
+            float(pb_c_base),
+            float(pb_c_init),
+            float(discount),
+            idx.ctypes.data_as(C.c_void_p),
+            idy.ctypes.data_as(C.c_void_p),
+            act.ctypes.data_as(C.c_void_p),
+            MZ_MEM_HOST,
+        )
+        check(self._lib, rc, "batch_selection")
+        return idx.tolist(), idy.tolist(), act.reshape(B, N)
+
+    def batch_expansion_and_backup(self, hidden_state_index_x, discount, sampled_times, rewards, values,
+                                   policy_probs, beta):
+        ptrs, mem, keep = self._inputs(rewards, values, policy_probs, beta)
+        rc = self._lib.mz_expand_backup(
+            self._h, int(hidden_state_index_x), float(discount), int(sampled_times), ptrs[0], ptrs[1], ptrs[2],
+            ptrs[3], mem
+        )
+        check(self._lib, rc, "batch_expansion_and_backup")
+
+    # -- device-resident variants (no host synchronisation) ------------------------------------
+    def batch_selection_device(self, pb_c_base, pb_c_init, discount, out=None):
+        """Like batch_selection but returns device int32 tensors (idx_x [B], idy [B], actions [B,N])."""
+        B, N = self.root_num, self.agent_num
+        if out is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+            out = (
+                torch.empty(B, dtype=torch.int32, device=dev),
+                torch.empty(B, dtype=torch.int32, device=dev),
+                torch.empty(B, N, dtype=torch.int32, device=dev),
+            )
+        self._sync_stream()
+        rc = self._lib.mz_select(
+            self._h, float(pb_c_base), float(pb_c_init), float(discount),
+            C.c_void_p(out[0].data_ptr()), C.c_void_p(out[1].data_ptr()), C.c_void_p(out[2].data_ptr()),
+            MZ_MEM_DEVICE,
+        )
+        check(self._lib, rc, "batch_selection_device")
+        return out
+
+    def expansion_backup_selection_device(self, hidden_state_index_x, discount, sampled_times, rewards, values,
+                                          policy_probs, beta, pb_c_base, pb_c_init, out, pool=None,
+                                          gather_out=None):
+        """Fused expand+backup of simulation s and selection of s+1 (+ optional hidden-state gather)."""
+        ts = [_f32_dev(t) for t in (rewards, values, policy_probs, beta)]
+        self._sync_stream()
+        if pool is not None:
+            slot_stride = pool.stride(0) * pool.element_size()
+            row_bytes = pool[0, 0].numel() * pool.element_size()
+            pool_ptr = C.c_void_p(pool.data_ptr())
+            g_ptr = C.c_void_p(gather_out.data_ptr())
+        else:
+            slot_stride = row_bytes = 0
+            pool_ptr = g_ptr = None
+        rc = self._lib.mz_expand_backup_select(
+            self._h, int(hidden_state_index_x), float(discount), int(sampled_times),
+            *[C.c_void_p(t.data_ptr()) for t in ts], float(pb_c_base), float(pb_c_init),
+            C.c_void_p(out[0].data_ptr()), C.c_void_p(out[1].data_ptr()), C.c_void_p(out[2].data_ptr()),
+            pool_ptr, int(slot_stride), int(row_bytes), g_ptr,
+        )
+        check(self._lib, rc, "expansion_backup_selection_device")
+        return out
+
+    # -- readbacks (cytree.pyx:93-241) ----------------------------------------------------------
+    def get_roots_values(self):
+        out = np.empty(self.root_num, np.float32)
+        check(self._lib, self._lib.mz_get_roots_values(self._h, out.ctypes.data_as(C.c_void_p), MZ_MEM_HOST),
+              "get_roots_values")
+        return out
+
+    def get_roots_marginal_visit_count(self):
+        out = np.empty(self.root_num * self.agent_num * self.action_space_size, np.int32)
+        check(self._lib, self._lib.mz_get_roots_marginal_visit_count(self._h, out.ctypes.data_as(C.c_void_p),
+                                                                      MZ_MEM_HOST), "get_roots_marginal_visit_count")
+        return out.reshape(self.root_num, self.agent_num, self.action_space_size)
+
+    def get_roots_marginal_priors(self):
+        out = np.empty(self.root_num * self.agent_num * self.action_space_size, np.float32)
+        check(self._lib, self._lib.mz_get_roots_marginal_priors(self._h, out.ctypes.data_as(C.c_void_p),
+                                                                 MZ_MEM_HOST), "get_roots_marginal_priors")
+        return out.reshape(self.root_num, self.agent_num, self.action_space_size)
+
+    def max_children(self) -> int:
+        if self._maxdeg is None:
+            v = C.c_int32()
+            check(self._lib, self._lib.mz_max_children(self._h, C.byref(v)), "max_children")
+            self._maxdeg = max(1, v.value)
+        return self._maxdeg
+
+    def get_roots_sampled_padded(self, name: str, discount: float = 0.0):
+        """One batched readback: (array [B, maxdeg(, N)], degrees [B])."""
+        B, N = self.root_num, self.agent_num
+        W = self.max_children()
+        dt = np.int32 if name in INT_FIELDS else np.float32
+        width = W * N if name == "actions" else W
+        out = np.zeros(B * width, dt)
+        deg = np.zeros(B, np.int32)
+        rc = self._lib.mz_get_roots_sampled_padded(
+            self._h, FIELDS[name], float(discount), out.ctypes.data_as(C.c_void_p), deg.ctypes.data_as(C.c_void_p),
+            MZ_MEM_HOST,
+        )
+        check(self._lib, rc, f"get_roots_sampled_{name}")
+        return out.reshape(B, width), deg
+
+    def _sampled_lists(self, name, discount=0.0):
+        arr, deg = self.get_roots_sampled_padded(name, discount)
+        if name == "actions":
+            N = self.agent_num
+            return [np.ascontiguousarray(arr[i, : deg[i] * N]).reshape(deg[i], N) for i in range(self.root_num)]
+        return [np.ascontiguousarray(arr[i, : deg[i]]) for i in range(self.root_num)]
+
+    def get_roots_sampled_visit_count(self):
+        return self._sampled_lists("visit_count")
+
+    def get_roots_sampled_actions(self):
+        return self._sampled_lists("actions")
+
+    def get_roots_sampled_pred_probs(self):
+        return self._sampled_lists("pred_probs")
+
+    def get_roots_sampled_beta(self):
+        return self._sampled_lists("beta")
+
+    def get_roots_sampled_beta_hat(self):
+        return self._sampled_lists("beta_hat")
+
+    def get_roots_sampled_priors(self):
+        return self._sampled_lists("priors")
+
+    def get_roots_sampled_imp_ratio(self):
+        return self._sampled_lists("imp_ratio")
+
+    def get_roots_sampled_pred_values(self):
+        return self._sampled_lists("pred_values")
+
+    def get_roots_sampled_mcts_values(self):
+        return self._sampled_lists("mcts_values")
+
+    def get_roots_sampled_rewards(self):
+        return self._sampled_lists("rewards")
+
+    def get_roots_sampled_qvalues(self, discount):
+        return self._sampled_lists("qvalues", discount)
+
+    # -- diagnostics ------------------------------------------------------------------------------
+    def stats(self) -> dict:
+        out = (C.c_int64 * _capi_stats_count())()
+        check(self._lib, self._lib.mz_get_stats(self._h, out), "stats")
+        return dict(zip(_capi.STATS, list(out)))
+
+    def synchronize(self):
+        check(self._lib, self._lib.mz_synchronize(self._h), "synchronize")
+
+    def print(self):
+        self._lib.mz_print(self._h)
+
+
+def _capi_stats_count() -> int:
+    return len(_capi.STATS)

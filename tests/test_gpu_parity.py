@@ -1,0 +1,233 @@
+"""Parity of the HIP product against the oracle (needs an MI355X: `pytest -m gpu`).
+
+Bar (BASELINE.json north_star): selection indices / actions and visit counts
+bit-exact; every float readback bit-exact too (the kernels replay the reference's f32/f64 op
+order), which is stronger than the 1e-5 Q tolerance the north star allows.
+
+* every committed golden trace (recorded from the compiled reference) through the host-memory
+  path, the device-tensor path and the fused device loop
+* BASELINE-size searches (256 roots x 50 sims, 1024 x 50, 512 x 100, 256 x 200) against the CPU
+  port, plus size-independent properties
+* sharded batches (root_offset) identical to the unsharded batch
+* gather kernel, device readbacks, error reporting
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_same, golden_traces, load_trace
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def gpu_lib():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    from mazero_amd._lib import load
+
+    return load()
+
+
+def make_tb(lib, inp, K, knobs, **kw):
+    from mazero_amd.cytree import Tree_batch
+
+    return Tree_batch(inp.B, 1, inp.A, K, inp.S, knobs.get("delta_lb", 0.01), inp.seed, knobs.get("rho", 0.75),
+                      knobs.get("lam", 0.8), lib=lib, **kw)
+
+
+def to_device(inp):
+    from dataclasses import replace
+
+    dev = torch.device("cuda")
+    f = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    return replace(inp, root_reward=f(inp.root_reward), root_value=f(inp.root_value), root_policy=f(inp.root_policy),
+                   root_beta=f(inp.root_beta), root_noise=f(inp.root_noise), reward=f(inp.reward),
+                   value=f(inp.value), policy=f(inp.policy), beta=f(inp.beta))
+
+
+def run_fused(tb, dinp, K, knobs, pool=None):
+    """The device-resident loop: prepare, select(0), then per simulation one fused
+    expand+backup+select(+gather) launch; selections are recorded on the device."""
+    from mazero_amd.synthetic import DEFAULTS, readbacks
+
+    k = dict(DEFAULTS)
+    k.update(knobs)
+    c2, c1, g = k["pb_c_base"], k["pb_c_init"], k["discount"]
+    B, S = dinp.B, dinp.S
+    dev = torch.device("cuda")
+    tb.prepare(dinp.root_reward, dinp.root_value, dinp.root_policy, dinp.root_beta, K, dinp.noise_eps,
+               dinp.root_noise)
+    idx = torch.empty(S, B, dtype=torch.int32, device=dev)
+    idy = torch.empty(S, B, dtype=torch.int32, device=dev)
+    act = torch.empty(S, B, 1, dtype=torch.int32, device=dev)
+    gathered = None
+    if pool is not None:
+        gathered = torch.empty((S,) + tuple(pool.shape[1:]), dtype=pool.dtype, device=dev)
+    tb.batch_selection_device(c2, c1, g, out=(idx[0], idy[0], act[0]))
+    if pool is not None:
+        tb._lib.mz_gather_rows(tb._h, pool.data_ptr(), pool.stride(0) * pool.element_size(),
+                               pool[0, 0].numel() * pool.element_size(), idx[0].data_ptr(), gathered[0].data_ptr())
+    for s in range(S):
+        if s + 1 < S:
+            tb.expansion_backup_selection_device(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s],
+                                                 dinp.beta[s], c2, c1, out=(idx[s + 1], idy[s + 1], act[s + 1]),
+                                                 pool=pool, gather_out=None if pool is None else gathered[s + 1])
+        else:
+            tb.batch_expansion_and_backup(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s], dinp.beta[s])
+    torch.cuda.synchronize()
+    out = dict(sel_idx=idx.cpu().numpy(), sel_act=act.cpu().numpy()[:, :, 0])
+    assert (idy.cpu().numpy() == np.arange(B, dtype=np.int32)[None]).all()
+    out.update(readbacks(tb, g))
+    return out, gathered
+
+
+TRACES = golden_traces()
+IDS = [os.path.basename(p)[6:-4] for p in TRACES]
+
+
+@pytest.mark.parametrize("path", TRACES, ids=IDS)
+def test_golden_host_path(gpu_lib, path):
+    from mazero_amd.synthetic import run_search
+
+    inp, knobs, K, expected = load_trace(path)
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    assert_same(run_search(tb, inp, K, knobs), expected, "gpu(host) ")
+
+
+@pytest.mark.parametrize("path", TRACES, ids=IDS)
+def test_golden_device_tensors(gpu_lib, path):
+    from mazero_amd.synthetic import run_search
+
+    inp, knobs, K, expected = load_trace(path)
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    assert_same(run_search(tb, to_device(inp), K, knobs), expected, "gpu(device) ")
+
+
+@pytest.mark.parametrize("path", TRACES, ids=IDS)
+def test_golden_fused_loop(gpu_lib, path):
+    inp, knobs, K, expected = load_trace(path)
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    out, _ = run_fused(tb, to_device(inp), K, knobs)
+    expected = {k: v for k, v in expected.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, expected, "gpu(fused) ")
+
+
+BIG = [
+    ("3m_k1", 256, 9, 1, 50, 0.0),
+    ("3m_k5", 256, 9, 5, 50, 0.3),
+    ("3m_k10", 256, 9, 10, 50, 0.0),
+    ("2s3z_k5", 1024, 11, 5, 50, 0.0),
+    ("3s5z_k5", 512, 15, 5, 100, 0.3),
+    ("27m_k1", 256, 36, 1, 200, 0.0),
+    ("27m_k5", 256, 36, 5, 200, 0.0),
+]
+
+
+@pytest.mark.parametrize("name,B,A,K,S,lz", BIG, ids=[b[0] for b in BIG])
+def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    rng = np.random.default_rng(hash(name) % 2**32)
+    inp = make_search_inputs(rng, B, A, S, legal_zero_frac=lz)
+    knobs = {}
+    exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
+    out, _ = run_fused(make_tb(gpu_lib, inp, K, knobs), to_device(inp), K, knobs)
+    exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, exp, f"gpu {name} ")
+    # size-independent properties (hold for the reference by construction)
+    vc = out["sampled_visit_count"].sum(axis=1)
+    assert (vc == S).all()  # every simulation passes through exactly one root child
+    assert (out["marginal_visit_count"].sum(axis=(1, 2)) == S).all()
+    deg = out["degree"]
+    assert (deg >= 1).all() and (deg <= min(K, A)).all()
+    bh = out["sampled_beta_hat"].sum(axis=1)
+    assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
+
+
+def test_gather_pool(gpu_lib):
+    """Fused leaf hidden-state gather == pool[idx_x[i], i] (mcts_sampled.py:130-134)."""
+    from mazero_amd.synthetic import make_search_inputs
+
+    B, A, K, S, H = 64, 9, 5, 20, 384
+    inp = make_search_inputs(np.random.default_rng(3), B, A, S)
+    pool = torch.randn(S + 1, B, H, device="cuda")
+    out, gathered = run_fused(make_tb(gpu_lib, inp, K, {}), to_device(inp), K, {}, pool=pool)
+    idx = torch.from_numpy(out["sel_idx"]).long().cuda()
+    ref = pool[idx, torch.arange(B, device="cuda")[None, :]]
+    assert torch.equal(gathered, ref)
+    # fp16 pools (autocast) gather the same bytes
+    pool16 = pool.half()
+    g16 = torch.empty(B, H, dtype=torch.float16, device="cuda")
+    tb = make_tb(gpu_lib, inp, K, {})
+    gpu_lib.mz_gather_rows(tb._h, pool16.data_ptr(), pool16.stride(0) * 2, H * 2, idx[3].int().contiguous().data_ptr(),
+                           g16.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(g16, pool16[idx[3], torch.arange(B, device="cuda")])
+
+
+def test_sharded_equals_unsharded(gpu_lib):
+    """Roots split over two handles with root_offset (one per rank in a multi-GPU job) give the
+    bit-identical trees of one unsharded batch (seed_i = random_seed*2333 + global index)."""
+    from dataclasses import replace
+
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    B, A, K, S = 96, 9, 5, 30
+    inp = make_search_inputs(np.random.default_rng(11), B, A, S)
+    full = run_search(make_tb(gpu_lib, inp, K, {}), inp, K)
+    h = B // 3
+    parts = []
+    for lo, hi in ((0, h), (h, B)):
+        sub = replace(inp, B=hi - lo, root_reward=inp.root_reward[lo:hi], root_value=inp.root_value[lo:hi],
+                      root_policy=inp.root_policy[lo:hi], root_beta=inp.root_beta[lo:hi],
+                      root_noise=inp.root_noise[lo:hi], reward=inp.reward[:, lo:hi], value=inp.value[:, lo:hi],
+                      policy=inp.policy[:, lo:hi], beta=inp.beta[:, lo:hi])
+        parts.append(run_search(make_tb(gpu_lib, sub, K, {}, root_offset=lo), sub, K))
+    for k in ("sel_idx", "sel_act", "root_values_per_sim"):
+        assert np.array_equal(np.concatenate([parts[0][k], parts[1][k]], axis=1), full[k]), k
+    for k in ("root_values", "marginal_visit_count", "sampled_visit_count", "sampled_qvalues"):
+        a, b = parts[0][k], parts[1][k]
+        w = max(a.shape[1], b.shape[1]) if a.ndim > 1 else None
+        if w is not None and a.ndim == 2:
+            a = np.pad(a, ((0, 0), (0, full[k].shape[1] - a.shape[1])))
+            b = np.pad(b, ((0, 0), (0, full[k].shape[1] - b.shape[1])))
+        assert np.array_equal(np.concatenate([a, b], axis=0), full[k]), k
+
+
+def test_device_readbacks(gpu_lib):
+    from mazero_amd._capi import MZ_MEM_DEVICE
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    B, A, K, S = 32, 9, 5, 20
+    inp = make_search_inputs(np.random.default_rng(5), B, A, S)
+    tb = make_tb(gpu_lib, inp, K, {})
+    ref = run_search(tb, inp, K)
+    v = torch.empty(B, device="cuda")
+    mv = torch.empty(B, 1, A, dtype=torch.int32, device="cuda")
+    assert gpu_lib.mz_get_roots_values(tb._h, v.data_ptr(), MZ_MEM_DEVICE) == 0
+    assert gpu_lib.mz_get_roots_marginal_visit_count(tb._h, mv.data_ptr(), MZ_MEM_DEVICE) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), ref["root_values"])
+    assert np.array_equal(mv.cpu().numpy(), ref["marginal_visit_count"])
+
+
+def test_too_many_simulations_raise(gpu_lib):
+    """The reference's pools are sized for simulation_num; overrunning them is reported as a
+    RuntimeError at the call that overflows (host path is synchronous like the reference)."""
+    from mazero_amd.cytree import Tree_batch
+
+    B, A, K, S = 4, 3, 1, 2
+    tb = Tree_batch(B, 1, A, K, S, 0.01, 5, 0.75, 0.8, lib=gpu_lib)
+    p = np.full((B, 1, A), 1.0 / A, np.float32)
+    z = np.zeros(B, np.float32)
+    tb.prepare(z, z, p, p, K, 0.0, p)
+    with pytest.raises(RuntimeError):
+        for s in range(10):
+            tb.batch_selection(19652.0, 1.25, 0.997)
+            tb.batch_expansion_and_backup(s + 1, 0.997, K, z, z, p, p)

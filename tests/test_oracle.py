@@ -1,0 +1,124 @@
+"""The oracle itself, pinned before it is trusted (CPU only).
+
+* libstdc++ known answers (tests/golden/kat_libstdcxx.json, made by oracle/kat_libstdcxx.cpp):
+  the restated std::mt19937 and std::discrete_distribution of oracle/ptree.py
+* the golden traces (tests/golden/trace_*.npz, recorded from the compiled reference ctree by
+  oracle/gen_golden.py) replayed through the pure-Python ptree and the C++ CPU port
+* the reference oracle itself, when it is built here, reproduces the committed traces
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, assert_same, golden_traces, load_trace
+
+import ptree
+from mazero_amd.cytree import Tree_batch
+from mazero_amd.synthetic import make_search_inputs, run_search
+
+
+@pytest.fixture(scope="module")
+def kat():
+    with open(os.path.join(GOLDEN, "kat_libstdcxx.json")) as f:
+        return json.load(f)
+
+
+def test_mt19937_known_answers(kat):
+    for seed, words in kat["mt"]:
+        g = ptree.MT19937(seed)
+        assert [g() for _ in range(len(words))] == words, f"seed {seed}"
+    g = ptree.MT19937(5489)
+    for _ in range(9999):
+        g()
+    assert g() == kat["mt10000_5489"] == 4123659995  # C++ standard [rand.predef]/3
+
+
+def test_discrete_distribution_known_answers(kat):
+    for seed, weights, draws, consumed in kat["dd"]:
+        w = np.asarray(weights, np.float32)
+        g = ptree.MT19937(seed)
+        d = ptree.Discrete(w)
+        got = [d(g) for _ in range(len(draws))]
+        assert got == draws, f"seed {seed} weights {weights}"
+        assert consumed == (0 if len(w) < 2 else 2 * len(draws))
+
+
+def test_pbc_table_known_answers(kat):
+    """glibc logf as ucb_score evaluates it (cnode.cpp:313)."""
+    libm = C.CDLL("libm.so.6")
+    libm.logf.restype = C.c_float
+    libm.logf.argtypes = [C.c_float]
+    f32 = np.float32
+    for c2, c1, n, bits in kat["pbc_logf_bits"]:
+        x = f32(f32(f32(n) + f32(c2)) + f32(1.0))
+        v = f32(f32(libm.logf(float(f32(x / f32(c2))))) + f32(c1))
+        assert int(v.view(np.uint32)) == bits
+
+
+@pytest.mark.parametrize("path", golden_traces(), ids=lambda p: os.path.basename(p)[6:-4])
+def test_port_matches_golden(path, port_lib):
+    inp, knobs, K, expected = load_trace(path)
+    tb = Tree_batch(inp.B, 1, inp.A, K, inp.S, knobs["delta_lb"], inp.seed, knobs["rho"], knobs["lam"], lib=port_lib)
+    assert_same(run_search(tb, inp, K, knobs), expected, "port ")
+
+
+SMALL = [p for p in golden_traces() if not any(s in p for s in ("deep", "27m_k5"))]
+
+
+@pytest.mark.parametrize("path", SMALL, ids=lambda p: os.path.basename(p)[6:-4])
+def test_ptree_matches_golden(path):
+    inp, knobs, K, expected = load_trace(path)
+    tb = ptree.Tree_batch(inp.B, 1, inp.A, K, inp.S, knobs["delta_lb"], inp.seed, knobs["rho"], knobs["lam"])
+    assert_same(run_search(tb, inp, K, knobs), expected, "ptree ")
+
+
+@pytest.mark.parametrize("path", golden_traces()[:4], ids=lambda p: os.path.basename(p)[6:-4])
+def test_reference_reproduces_golden(path, ref_lib):
+    inp, knobs, K, expected = load_trace(path)
+    tb = Tree_batch(inp.B, 1, inp.A, K, inp.S, knobs["delta_lb"], inp.seed, knobs["rho"], knobs["lam"], lib=ref_lib)
+    assert_same(run_search(tb, inp, K, knobs), expected, "ref ")
+
+
+@pytest.mark.parametrize("K,A,ties,lz", [(1, 9, False, 0.0), (5, 9, False, 0.3), (10, 15, True, 0.0)])
+def test_port_matches_reference_fresh(ref_lib, port_lib, K, A, ties, lz):
+    """Beyond the committed traces: fresh random searches, reference vs port, bit-exact."""
+    rng = np.random.default_rng(K * 100 + A)
+    inp = make_search_inputs(rng, 32, A, 50, legal_zero_frac=lz, ties=ties)
+    outs = []
+    for lib in (ref_lib, port_lib):
+        tb = Tree_batch(inp.B, 1, A, K, inp.S, 0.01, inp.seed, 0.75, 0.8, lib=lib)
+        outs.append(run_search(tb, inp, K))
+    assert_same(outs[1], outs[0], "port vs ref ")
+
+
+def test_ptree_joint_action_matches_reference(ref_lib):
+    """agent_num = 2 joint-action trees (upstream MAZero semantics)."""
+    rng = np.random.default_rng(7)
+    B, N, A, K, S = 4, 2, 3, 5, 20
+    pol = rng.dirichlet([1.0] * A, (B, N)).astype(np.float32)
+    noise = rng.dirichlet([0.3] * A, (B, N)).astype(np.float32)
+    r = np.zeros(B, np.float32)
+    v = rng.standard_normal(B).astype(np.float32)
+    trees = [Tree_batch(B, N, A, K, S, 0.01, 11, 0.75, 0.8, lib=ref_lib),
+             ptree.Tree_batch(B, N, A, K, S, 0.01, 11, 0.75, 0.8)]
+    res = [[], []]
+    for k, tb in enumerate(trees):
+        tb.prepare(r, v, pol, pol, K, 0.25, noise)
+        for s in range(S):
+            ix, _, act = tb.batch_selection(19652.0, 1.25, 0.997)
+            res[k].append((list(ix), np.asarray(act).tolist()))
+            p = rng.dirichlet([1.0] * A, (B, N)).astype(np.float32) if k == 0 else saved[s][0]
+            if k == 0:
+                saved.append((p,))
+            tb.batch_expansion_and_backup(s + 1, 0.997, K, r, v, p, p)
+        res[k].append(tb.get_roots_marginal_visit_count().tolist())
+        res[k].append(tb.get_roots_values().tolist())
+    assert res[0] == res[1]
+
+
+saved = []
