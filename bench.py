@@ -227,6 +227,9 @@ def main():
             avg_launch_us=round(avg * 1e6, 3),
             mean_path_len=round(st["path_edges"] / max(1, st["selects"]), 3),
         )
+        if os.environ.get("MZ_STAMPS") == "1" and st.get("stamped", 0) > 0:
+            # diagnostic build: average shader cycles per fused launch and tree, per phase
+            roofline["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

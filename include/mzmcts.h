@@ -75,7 +75,19 @@ enum mz_stat {
     MZ_S_ENTRIES_READ = 6,   /* value-set entries scanned by back-propagation              */
     MZ_S_ENTRIES_WRITTEN = 7,/* value-set entries written by back-propagation              */
     MZ_S_MINMAX_NODES = 8,   /* node q-values scanned for the min/max normaliser           */
-    MZ_S_COUNT = 9
+    /* Diagnostic builds only (compiled with MZ_STAMPS=1; zero otherwise): shader cycles spent in
+     * each phase of the fused simulation-step kernel, summed over trees and launches. */
+    MZ_S_CYC_HEADER = 9,     /* tree header load                                           */
+    MZ_S_CYC_STAGE1 = 10,    /* tables, path, network outputs -> LDS                       */
+    MZ_S_CYC_STAGE2 = 11,    /* node records, q, path scalars, RNG window -> LDS           */
+    MZ_S_CYC_EXPAND = 12,    /* leaf expansion                                             */
+    MZ_S_CYC_BACKUP = 13,    /* back-propagation (bootstrap + value sets)                  */
+    MZ_S_CYC_MINMAX = 14,    /* min/max normaliser                                         */
+    MZ_S_CYC_SELECT = 15,    /* selection walk                                             */
+    MZ_S_CYC_GATHER = 16,    /* hidden-state gather                                        */
+    MZ_S_CYC_EPILOGUE = 17,  /* header / path write-back                                   */
+    MZ_S_STAMPED = 18,       /* stamped launches x trees                                   */
+    MZ_S_COUNT = 19
 };
 
 /* --- library -------------------------------------------------------------------------- */

@@ -38,6 +38,16 @@ STATS = [
     "entries_read",
     "entries_written",
     "minmax_nodes",
+    "cyc_header",
+    "cyc_stage1",
+    "cyc_stage2",
+    "cyc_expand",
+    "cyc_backup",
+    "cyc_minmax",
+    "cyc_select",
+    "cyc_gather",
+    "cyc_epilogue",
+    "stamped",
 ]
 
 EXPORTS = [

@@ -11,28 +11,30 @@ import os
 import threading
 
 from . import _capi
-from .build import LIB
+from .build import LIB, LIB_STAMPS
 
 _lock = threading.Lock()
 _lib = None
 
 
 def load() -> C.CDLL:
+    """The product library; MZ_STAMPS=1 in the environment selects the diagnostic build."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
+        path = LIB_STAMPS if os.environ.get("MZ_STAMPS") == "1" else LIB
         try:
             import torch  # noqa: F401  (plumbing: share torch's HIP runtime)
         except Exception:
             pass
-        if not os.path.exists(LIB):
+        if not os.path.exists(path):
             raise RuntimeError(
-                f"MI355X library not built: {LIB} is missing (run `python -m mazero_amd.build` "
+                f"MI355X library not built: {path} is missing (run `python -m mazero_amd.build` "
                 "or __graft_entry__.build())"
             )
-        lib = _capi.bind(C.CDLL(LIB, mode=C.RTLD_LOCAL))
+        lib = _capi.bind(C.CDLL(path, mode=C.RTLD_LOCAL))
         if lib.mz_abi_version() != 1 or lib.mz_backend() != b"hip-gfx950":
-            raise RuntimeError(f"{LIB} is not the hip-gfx950 backend of ABI 1")
+            raise RuntimeError(f"{path} is not the hip-gfx950 backend of ABI 1")
         _lib = lib
         return lib

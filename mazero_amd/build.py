@@ -20,6 +20,7 @@ ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "mzmcts.hip")
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libmzmcts.so")
+LIB_STAMPS = os.path.join(OUT_DIR, "libmzmcts_stamps.so")  # diagnostic build (MZ_STAMPS=1)
 ARCH = os.environ.get("MZ_OFFLOAD_ARCH", "gfx950")
 
 FLAGS = [
@@ -43,26 +44,33 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: the MI355X library cannot be built")
 
 
-def needs_build() -> bool:
-    if not os.path.exists(LIB):
+def needs_build(lib: str = LIB) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [SRC, os.path.join(ROOT, "include", "mzmcts.h"), __file__]
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
-        return LIB
+def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> str:
+    lib = LIB_STAMPS if stamps else LIB
+    if not force and not needs_build(lib):
+        return lib
     os.makedirs(OUT_DIR, exist_ok=True)
-    tmp = LIB + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp]
+    tmp = lib + ".tmp"
+    extra = ["-DMZ_STAMPS=1"] if stamps else []
+    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp]
     if verbose:
         print("[mazero_amd] " + " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
+
+
+def build_all(force: bool = False, verbose: bool = True) -> None:
+    build(force=force, verbose=verbose)
+    build(force=force, verbose=verbose, stamps=True)
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build_all(force="--force" in sys.argv)

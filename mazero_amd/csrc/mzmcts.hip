@@ -40,6 +40,10 @@
 
 namespace {
 
+#ifndef MZ_STAMPS
+#define MZ_STAMPS 0  // diagnostic build: per-phase s_memtime stamps into the stats counters
+#endif
+
 constexpr int kWave = 64;
 constexpr int kRngWin = 256;     // RNG words staged in LDS per launch
 constexpr int kMaxActions = 64;  // one lane per action
@@ -133,6 +137,15 @@ __device__ __forceinline__ void glds4(const void *src, void *lds_base) {
 }
 __device__ __forceinline__ void glds16(const void *src, void *lds_base) {
     __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)lds_base, 16, 0, 0);
+}
+
+// Phase stamp (diagnostic builds): drain this wave's memory traffic, then read the shader clock.
+__device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
+    if constexpr (MZ_STAMPS != 0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        ts[i] = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
 }
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -400,7 +413,7 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
 // over the q of every visited non-root node -- exactly the multiset's content.
 // --------------------------------------------------------------------------------------------
 __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float disc, TreeHdr &h,
-                       int &err, long long *stl) {
+                       int &err, long long *stl, unsigned long long *ts) {
     const int l = lane_id();
     // bootstrap values (cnode.cpp:424,448)
     {
@@ -515,6 +528,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         i0 += cnt;
     }
     stl[MZ_S_BACKUP_NODES] += D + 1;
+    stamp(ts, 5);
     // min/max over the q of visited non-root nodes
     float mn = INFINITY, mx = -INFINITY;
     int cv = 0;
@@ -643,7 +657,10 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     Lds s(smem, g);
     const int t = blockIdx.x;
     const int l = threadIdx.x;
+    unsigned long long ts[10] = {0};
+    stamp(ts, 0);
     TreeHdr h = d.hdr[t];
+    stamp(ts, 1);
     if (h.err) {
         if (SEL && l == 0) {
             a.idx_x[t] = 0;
@@ -677,6 +694,7 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         v_in = a.value[t];
     }
     wait_vm();
+    stamp(ts, 2);
 
     // ---- round 2: node records, q, path-node value scalars, RNG window ----
     const int tot = h.tot;
@@ -694,6 +712,7 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     for (int i = l; i < kRngWin; i += kWave)
         if (wbase + i < g.W) glds4(d.R + (size_t)t * g.W + wbase + i, s.rng + (i - l));
     wait_vm();
+    stamp(ts, 3);
 
     int cursor = h.cursor;
     int ntot = tot;
@@ -716,12 +735,14 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
             d.Bn[nb + leaf] = nbv;
         }
         wait_lds();
+        stamp(ts, 4);
         if (!err) {
             h.cursor = cursor;
             h.tot = ntot;
-            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, err, stl);
+            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, err, stl, ts);
         }
     }
+    stamp(ts, 6);
     if (SEL && !err) {
         int idx = 0, act = 0;
         select_walk(g, d, s, t, a.discount, h, wbase, err, idx, act, stl);
@@ -730,6 +751,7 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
             a.idy[t] = t;
             a.act[t] = act;
         }
+        stamp(ts, 7);
         if (a.pool) {  // mcts_sampled.py:130-134: leaf hidden state = pool[idx_x][t]
             const char *src = a.pool + (long long)idx * a.pool_stride + (long long)t * a.row_bytes;
             char *dst = a.gather_out + (long long)t * a.row_bytes;
@@ -746,9 +768,22 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         a.idy[t] = t;
         a.act[t] = 0;
     }
+    stamp(ts, 8);
     if (l == 0) {
         h.err = err;
         d.hdr[t] = h;
+    }
+    stamp(ts, 9);
+    if (MZ_STAMPS && EB && SEL && !err) {
+        // phases: header, stage1, stage2, expand, backup, minmax, select(+outputs), gather, epilogue
+        if (ts[4] == 0) ts[4] = ts[3];
+        if (ts[5] == 0) ts[5] = ts[4];
+        if (ts[6] == 0) ts[6] = ts[5];
+        if (ts[7] == 0) ts[7] = ts[6];
+        for (int k = 0; k < 9; ++k) stl[MZ_S_CYC_HEADER + k] += (long long)(ts[k + 1] - ts[k]);
+        stl[MZ_S_STAMPED] += 1;
+    }
+    if (l == 0) {
         long long *st = d.stats + (size_t)t * MZ_S_COUNT;
 #pragma unroll
         for (int k = 0; k < MZ_S_COUNT; ++k) st[k] += stl[k];
