@@ -114,24 +114,29 @@ typedef __attribute__((address_space(1))) void glb_void;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ float i2f(int x) { return __int_as_float(x); }
+__device__ __forceinline__ int f2i(float x) { return __float_as_int(x); }
+// Cross-lane reads.  Values read from LDS are divergent for the compiler even when every lane read
+// the same address; uni() states the uniformity (v_readfirstlane), so wave-uniform state lives in
+// SGPRs and uniform control flow compiles to scalar branches instead of exec-mask juggling.
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float unif(float v) { return i2f(uni(f2i(v))); }
+__device__ __forceinline__ int4 uni4(int4 v) { return make_int4(uni(v.x), uni(v.y), uni(v.z), uni(v.w)); }
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float rlf(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
+__device__ __forceinline__ float rlf(float v, int l) { return i2f(__builtin_amdgcn_readlane(f2i(v), l)); }
 __device__ __forceinline__ double rld(double v, int l) {
     const long long b = __double_as_longlong(v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffll), l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-__device__ __forceinline__ float i2f(int x) { return __int_as_float(x); }
-__device__ __forceinline__ int f2i(float x) { return __float_as_int(x); }
 
-// Wait for this wave's LDS traffic (LDS-DMA included via vmcnt) and fence the compiler.
+// Wait for this wave's memory traffic (LDS-DMA included via vmcnt) / LDS traffic; compiler fence.
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// LDS-DMA: lane l copies `bytes` (4 or 16) from its own src into lds_base + l*bytes.
+// LDS-DMA: lane l copies `bytes` (4 or 16) from its own src into lds_base + l*bytes (lds_base
+// must be wave-uniform).
 __device__ __forceinline__ void glds4(const void *src, void *lds_base) {
     __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)lds_base, 4, 0, 0);
 }
@@ -148,29 +153,32 @@ __device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
     }
 }
 
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int l = lane_id();
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-        const int u = __shfl_up(v, o, kWave);
-        if (l >= o) v += u;
-    }
-    return v;
-}
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+// Whole-wave reductions with DPP (no LDS round trips): xor-pairs, xor-quads, half-row and row
+// mirrors reduce each 16-lane row; the four row results are combined from SGPRs.
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
 }
 __device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
-    return v;
+    v = fminf(v, i2f(dpp<0xB1>(f2i(v))));   // quad_perm [1,0,3,2]
+    v = fminf(v, i2f(dpp<0x4E>(f2i(v))));   // quad_perm [2,3,0,1]
+    v = fminf(v, i2f(dpp<0x141>(f2i(v))));  // row_half_mirror
+    v = fminf(v, i2f(dpp<0x140>(f2i(v))));  // row_mirror
+    return fminf(fminf(rlf(v, 0), rlf(v, 16)), fminf(rlf(v, 32), rlf(v, 48)));
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-    return v;
+    v = fmaxf(v, i2f(dpp<0xB1>(f2i(v))));
+    v = fmaxf(v, i2f(dpp<0x4E>(f2i(v))));
+    v = fmaxf(v, i2f(dpp<0x141>(f2i(v))));
+    v = fmaxf(v, i2f(dpp<0x140>(f2i(v))));
+    return fmaxf(fmaxf(rlf(v, 0), rlf(v, 16)), fmaxf(rlf(v, 32), rlf(v, 48)));
+}
+__device__ __forceinline__ int wave_sum(int v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    v += dpp<0x140>(v);
+    return rl(v, 0) + rl(v, 16) + rl(v, 32) + rl(v, 48);
 }
 
 // size_lim of SubTreeValueSet::update (utils.cpp:31): max(1, (int)ceil(count * (1 - rho)))
@@ -180,7 +188,7 @@ __device__ __forceinline__ int value_lim(int c, float one_minus_rho) {
 }
 
 // --------------------------------------------------------------------------------------------
-// Stage: one tree's view of LDS
+// One tree's view of LDS
 // --------------------------------------------------------------------------------------------
 struct Lds {
     int4 *A, *B;
@@ -200,11 +208,11 @@ struct Lds {
           reg((int2 *)(s + g.oReg)) {}
 };
 
-// RNG word `idx` of tree t: from the LDS window [wbase, wbase+kRngWin) or from HBM.
-__device__ __forceinline__ unsigned rng_word(const Geo &g, const Dev &d, const unsigned *win, int wbase, int t,
-                                             int idx, int &err) {
+// RNG word `idx` (per lane) of tree t: LDS window [wbase, wbase+kRngWin) or HBM.
+__device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, const unsigned *win, int wbase, int t,
+                                                  int idx, int &err) {
     const int o = idx - wbase;
-    if (o >= 0 && o < kRngWin && win) return win[o];
+    if (win && o >= 0 && o < kRngWin) return win[o];
     if (idx >= g.W) {
         err |= kErrRng;
         return 0u;
@@ -219,7 +227,8 @@ __device__ __forceinline__ unsigned rng_word(const Geo &g, const Dev &d, const u
 // std::discrete_distribution<int> + generate_canonical<double,53> (libstdc++ random.tcc:
 // 2656-2713, 3348-3378): double prefix sums of beta/sum(beta), last forced to 1.0; two engine words
 // per draw; index = lower_bound.  Fewer than two actions => no draw and no engine word.
-// Returns nc; writes the children to HBM (and to the LDS mirrors when given).
+// Creates the children in HBM (and in the LDS mirrors when given), advances cursor / tot and
+// returns nc.
 // --------------------------------------------------------------------------------------------
 __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float bet, float noi, float eps, int K,
                            int &cursor, int &tot, const unsigned *win, int wbase, int4 *sA, int4 *sB, float *sQ,
@@ -230,7 +239,7 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
     if (A < 2) {
         cnt = (l == 0) ? K : 0;
     } else {
-        // cumulative distribution (param_type::_M_initialize)
+        // cumulative distribution (param_type::_M_initialize): sequential double sums
         const double bd = (l < A) ? (double)bet : 0.0;
         double sum = 0.0;
         for (int a = 0; a < A; ++a) sum += rld(bd, a);
@@ -248,8 +257,8 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
             int idx = 0;
             if (l < nk) {
                 const int w = cursor + 2 * (k0 + l);
-                const double w1 = (double)rng_word(g, d, win, wbase, t, w, err);
-                const double w2 = (double)rng_word(g, d, win, wbase, t, w + 1, err);
+                const double w1 = (double)rng_word_lane(g, d, win, wbase, t, w, err);
+                const double w2 = (double)rng_word_lane(g, d, win, wbase, t, w + 1, err);
                 double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
                 if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
                 for (int a = 0; a < A; ++a) idx += (rld(cp, a) < u) ? 1 : 0;
@@ -268,9 +277,9 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
     if (has) {
         const int rank = __popcll(m & ((1ull << l) - 1ull));
         const int c = tot + rank;
-        const float bh = (float)cnt / (float)K;              // betahat_prob = count / sampled_times
+        const float bh = (float)cnt / (float)K;  // betahat_prob = count / sampled_times
         float prior = (eps > 0) ? (pol * (1 - eps) + noi * eps) : pol;
-        prior = prior * bh / bet;                             // prior * betahat_prob / beta_prob
+        prior = prior * bh / bet;  // prior * betahat_prob / beta_prob
         const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
         const int4 b4 = make_int4(0, (l << 16), f2i(0.0f), -1);
         const size_t gi = (size_t)t * g.P + c;
@@ -404,16 +413,53 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
 }
 
 // --------------------------------------------------------------------------------------------
-// CTree::back_propagate (cnode.cpp:415-450) over the path held in LDS.  Lane i owns path node i
-// (chunks of <= 64 nodes whose value entries fit the LDS staging area).  Bootstrap values are a
-// sequential f32 recurrence b_{i-1} = reward_i + discount * b_i, computed once by the whole wave.
-// Each node's SubTreeValueSet::update (utils.cpp:20-71) reads min(big) / max(small) as order
-// statistics of its sorted entries at that depth and replays the reference's f32 op sequence.
-// Afterwards the min/max normaliser (CMinMaxStats, utils.cpp:79-103) is recomputed as a reduction
-// over the q of every visited non-root node -- exactly the multiset's content.
+// Back-propagation staging: the value entries of path nodes [i0, i0+cnt) -> LDS with LDS-DMA.
+// Chunks hold <= 64 nodes whose entries fit g.reg_cap.  Returns cnt (uniform); lane l gets its
+// node id, entry count (= visit at selection) and entry offset inside the staging area.
+// --------------------------------------------------------------------------------------------
+__device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &off) {
+    const int l = lane_id();
+    const int i = i0 + l;
+    n = 0;
+    nv = 0;
+    off = 0;
+    if (i <= D) {
+        const int2 pe = s.path[i];
+        n = pe.x;
+        nv = pe.y;
+    }
+    const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
+    int acc = 0, cnt = 0;
+    for (int j = 0; j < lim; ++j) {  // uniform prefix sum over the chunk
+        const int vj = rl(nv, j);
+        if (acc + vj > g.reg_cap) break;
+        if (l == j) off = acc;
+        acc += vj;
+        ++cnt;
+    }
+    const int2 *gV = d.V + (size_t)t * g.P * g.E;
+    int *regdw = (int *)s.reg;
+    for (int j = 0; j < cnt; ++j) {
+        const int nj = rl(n, j), vj = rl(nv, j), oj = rl(off, j);
+        const int dw = 2 * vj;
+        const int *src = (const int *)(gV + (size_t)nj * g.E);
+        for (int c = 0; c < dw; c += kWave)
+            if (c + l < dw) glds4(src + c + l, regdw + 2 * oj + c);
+    }
+    return cnt;
+}
+
+// --------------------------------------------------------------------------------------------
+// CTree::back_propagate (cnode.cpp:415-450) over the path held in LDS.  Lane i owns path node i.
+// Bootstrap values are a sequential f32 recurrence b_{i-1} = reward_i + discount * b_i, computed
+// once by the whole wave.  Each node's SubTreeValueSet::update (utils.cpp:20-71) reads min(big)
+// / max(small) as order statistics of its sorted entries at that depth and replays the
+// reference's f32 op sequence.  Afterwards the min/max normaliser (CMinMaxStats, utils.cpp:
+// 79-103) is recomputed as a reduction over the q of every visited non-root node -- exactly the
+// multiset's content.  Chunk 0's entries must already be in flight (stage_regions).
 // --------------------------------------------------------------------------------------------
 __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float disc, TreeHdr &h,
-                       int &err, long long *stl, unsigned long long *ts) {
+                       int cnt0, int n0, int nv0, int off0, int &err, long long *stl, unsigned long long *ts) {
     const int l = lane_id();
     // bootstrap values (cnode.cpp:424,448)
     {
@@ -431,45 +477,43 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             }
             if (l < n) s.boot[base - l - 1] = mine;
         }
-        wait_lds();
     }
     int2 *gV = d.V + (size_t)t * g.P * g.E;
+    int cnt = cnt0, n = n0, nv = nv0, off = off0;
+    long long ent_r = 0, ent_w = 0;
     for (int i0 = 0; i0 <= D;) {
-        const int i = i0 + l;
-        const bool act = i <= D;
-        const int2 pe = act ? s.path[i] : make_int2(0, 0);
-        const int n = pe.x, nv = pe.y;
-        const int inc = wave_incl_scan(act ? nv : 0);
-        const unsigned long long fm = ballot(act && inc <= g.reg_cap);
-        const int cnt = __popcll(fm);
         if (cnt == 0) {
             err |= kErrPath;
             return;
         }
-        const int off = inc - nv;
-        // stage the chunk's value entries with LDS-DMA (2 dwords per entry)
-        int *regdw = (int *)s.reg;
-        for (int j = 0; j < cnt; ++j) {
-            const int nj = rl(n, j), vj = rl(nv, j), oj = rl(off, j);
-            const int dw = 2 * vj;
-            const int *src = (const int *)(gV + (size_t)nj * g.E);
-            for (int c = 0; c < dw; c += kWave)
-                if (c + l < dw) glds4(src + c + l, regdw + 2 * oj + c);
-        }
         wait_vm();
+        wait_lds();
+        const int i = i0 + l;
         if (l < cnt) {
             const int dep = D - i;
             const float key = s.boot[i];
             const int2 *R = s.reg + off;
-            int lo = 0, c = 0, pv = 0;
-            for (int j = 0; j < nv; ++j) {
-                const int2 e = R[j];
-                lo += (e.x < dep) ? 1 : 0;
-                const bool eq = (e.x == dep);
-                c += eq ? 1 : 0;
-                pv += (eq && i2f(e.y) < key) ? 1 : 0;
+            int lo = nv, c = 0, pv = 0;
+            // entries are sorted by depth: a new deepest depth (always so in K=1 chains) needs no scan
+            if (nv > 0 && R[nv - 1].x >= dep) {
+                lo = 0;
+                int j = 0;
+                for (; j + 4 <= nv; j += 4) {
+                    const int2 e0 = R[j], e1 = R[j + 1], e2 = R[j + 2], e3 = R[j + 3];
+                    lo += (e0.x < dep) + (e1.x < dep) + (e2.x < dep) + (e3.x < dep);
+                    c += (e0.x == dep) + (e1.x == dep) + (e2.x == dep) + (e3.x == dep);
+                    pv += (e0.x == dep && i2f(e0.y) < key) + (e1.x == dep && i2f(e1.y) < key) +
+                          (e2.x == dep && i2f(e2.y) < key) + (e3.x == dep && i2f(e3.y) < key);
+                }
+                for (; j < nv; ++j) {
+                    const int2 e = R[j];
+                    lo += (e.x < dep);
+                    c += (e.x == dep);
+                    pv += (e.x == dep && i2f(e.y) < key);
+                }
+                ent_r += nv;
             }
-            float4 cw = s.C[i];
+            const float4 cw = s.C[i];
             float ws = cw.x, tw = cw.y;
             const float lp = s.lp[dep];
             const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
@@ -501,13 +545,13 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             // insert (dep, key) at its sorted place: shift the tail up by one in HBM
             const int pos = lo + pv;
             int2 *G = gV + (size_t)n * g.E;
-            if (nv + 1 > g.E) err |= kErrPath;
-            else {
+            if (nv + 1 > g.E) {
+                err |= kErrPath;
+            } else {
                 for (int j = nv - 1; j >= pos; --j) G[j + 1] = R[j];
                 G[pos] = make_int2(dep, f2i(key));
             }
-            stl[MZ_S_ENTRIES_READ] += nv;
-            stl[MZ_S_ENTRIES_WRITTEN] += nv - pos + 1;
+            ent_w += nv - pos + 1;
             // node scalars
             const int4 a4 = s.A[n];
             const int nc = s.B[n].y & 0xffff;
@@ -526,15 +570,19 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         }
         wait_lds();
         i0 += cnt;
+        if (i0 <= D) cnt = stage_regions(g, d, s, t, D, i0, n, nv, off);
     }
     stl[MZ_S_BACKUP_NODES] += D + 1;
+    stl[MZ_S_ENTRIES_READ] += ent_r;
+    stl[MZ_S_ENTRIES_WRITTEN] += ent_w;
     stamp(ts, 5);
     // min/max over the q of visited non-root nodes
     float mn = INFINITY, mx = -INFINITY;
     int cv = 0;
-    for (int n = 1 + l; n < tot; n += kWave) {
-        if (s.A[n].x > 0) {
-            const float q = s.Q[n];
+    for (int base = 1; base < tot; base += kWave) {
+        const int nn = base + l;
+        if (nn < tot && s.A[nn].x > 0) {
+            const float q = s.Q[nn];
             mn = fminf(mn, q);
             mx = fmaxf(mx, q);
             ++cv;
@@ -546,19 +594,52 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
     stl[MZ_S_MINMAX_NODES] += tot - 1;
 }
 
+// pUCT table entry n (uniform): lanes hold entries l, 64+l, 128+l, 192+l; larger n from LDS.
+struct PucTables {
+    float pb[4];
+    double sq[4];
+};
+__device__ __forceinline__ void puct_lookup(const PucTables &pt, const Lds &s, int n, float &pb, double &sq) {
+    const int r = n >> 6, o = n & 63;
+    if (r == 0) {
+        pb = rlf(pt.pb[0], o);
+        sq = rld(pt.sq[0], o);
+    } else if (r == 1) {
+        pb = rlf(pt.pb[1], o);
+        sq = rld(pt.sq[1], o);
+    } else if (r == 2) {
+        pb = rlf(pt.pb[2], o);
+        sq = rld(pt.sq[2], o);
+    } else if (r == 3) {
+        pb = rlf(pt.pb[3], o);
+        sq = rld(pt.sq[3], o);
+    } else {
+        pb = unif(s.pb[n]);
+        const double q = s.sq[n];
+        const long long qb = __double_as_longlong(q);
+        sq = __longlong_as_double(((long long)(unsigned)uni((int)(qb >> 32)) << 32) |
+                                  (unsigned)uni((int)(qb & 0xffffffffll)));
+    }
+}
+
 // --------------------------------------------------------------------------------------------
 // CTree::select_path (cnode.cpp:381-413) with select_child (337-379) and ucb_score (297-335),
 // walking the LDS copy.  Lane j scores child j; the arg-max with epsilon ties is the reference's
 // sequential scan over the lanes (uniform loop), one engine word when the tie list is non-empty.
+// All walk state is wave-uniform (SGPRs).  RNG words come from two registers holding the window
+// [wbase, wbase+128) (lane j: words j and 64+j), then the LDS window, then HBM.
 // --------------------------------------------------------------------------------------------
-__device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float disc, TreeHdr &h, int wbase, int &err,
-                            int &out_idx, int &out_act, long long *stl) {
+__device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float disc, TreeHdr &h, int lds_base,
+                            unsigned rw0, unsigned rw1, const PucTables &pt, int &err, int &out_idx, int &out_act,
+                            long long *stl) {
+    const int wbase = h.cursor;  // register window [wbase, wbase + 128)
     const int l = lane_id();
     int x = 0;
-    int4 xa = s.A[0];
-    int4 xb = s.B[0];
-    int4 pb_ = xb;  // parent's B (for hidden_state_index_x)
+    int4 xa = uni4(s.A[0]);
+    int4 xb = uni4(s.B[0]);
+    int phsx = xb.w;  // hidden_state_index_x of the current node's parent
     int D = 0;
+    int cursor = h.cursor;
     if (l == 0) s.path[0] = make_int2(0, xa.x);
     const bool mm_on = h.mm_cnt > 0;
     const float mmn = h.mm_min, mmx = h.mm_max;
@@ -574,9 +655,12 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
         const int fc = xb.x;
         // every lane reads its child's records (one LDS round trip per level)
         const bool has = l < nc;
-        const int4 ca = has ? s.A[fc + l] : make_int4(0, 0, 0, 0);
-        const int4 cb = has ? s.B[fc + l] : make_int4(0, 0, 0, 0);
-        int ci;
+        int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
+        if (has) {
+            ca = s.A[fc + l];
+            cb = s.B[fc + l];
+        }
+        int ci = 0;
         if (x == 0 && xa.x <= nc) {
             ci = xa.x - 1;  // forced root round-robin (cnode.cpp:398-399)
         } else {
@@ -585,15 +669,17 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
                 err |= kErrTable;
                 break;
             }
-            const float pbl = s.pb[ntot];
-            const double sqn = s.sq[ntot];
+            float pbl;
+            double sqn;
+            puct_lookup(pt, s, ntot, pbl, sqn);
+            const float ppv = i2f(xb.z);
             float score = 0.f;
             if (has) {
                 const int v = ca.x;
                 float pbc = pbl;
                 pbc = (float)((double)pbc * (sqn / (double)(v + 1)));
                 const float prior_score = pbc * i2f(ca.y);
-                float vs = (v == 0) ? 0.0f : ((i2f(ca.w) + disc * i2f(ca.z)) - i2f(xb.z));
+                float vs = (v == 0) ? 0.0f : ((i2f(ca.w) + disc * i2f(ca.z)) - ppv);
                 if (mm_on) vs = (vs - mmn) / den;
                 if (vs < 0) vs = 0;
                 if (vs > 1) vs = 1;
@@ -611,18 +697,27 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
                     lst |= 1ull << j;
                 }
             }
-            ci = 0;
             const int cnt = __popcll(lst);
             if (cnt > 0) {
-                const unsigned w = rng_word(g, d, s.rng, wbase, t, h.cursor, err);
-                h.cursor += 1;
-                int k = (int)(w % (unsigned)cnt);
+                const int o = cursor - wbase;
+                unsigned w;
+                if (o >= 0 && o < kWave) w = (unsigned)rl((int)rw0, o);
+                else if (o >= kWave && o < 2 * kWave) w = (unsigned)rl((int)rw1, o - kWave);
+                else if (cursor - lds_base >= 0 && cursor - lds_base < kRngWin)
+                    w = (unsigned)uni((int)s.rng[cursor - lds_base]);
+                else if (cursor < g.W) w = (unsigned)uni((int)d.R[(size_t)t * g.W + cursor]);
+                else {
+                    err |= kErrRng;
+                    w = 0u;
+                }
+                ++cursor;
+                int k = (cnt == 1) ? 0 : (int)(w % (unsigned)cnt);  // gen() % max_index_lst.size()
                 for (; k > 0; --k) lst &= lst - 1ull;
                 ci = __builtin_ctzll(lst);
             }
         }
         // descend
-        pb_ = xb;
+        phsx = xb.w;
         x = fc + ci;
         xa = make_int4(rl(ca.x, ci), rl(ca.y, ci), rl(ca.z, ci), rl(ca.w, ci));
         xb = make_int4(rl(cb.x, ci), rl(cb.y, ci), rl(cb.z, ci), rl(cb.w, ci));
@@ -634,9 +729,10 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
         if (l == 0) s.path[D] = make_int2(x, xa.x);
     }
     if (D == 0) err |= kErrRoot;
+    h.cursor = cursor;
     h.D = D;
     h.leaf = x;
-    out_idx = pb_.w;       // parent->hidden_state_index_x
+    out_idx = phsx;        // parent->hidden_state_index_x
     out_act = xb.y >> 16;  // children_action of the last edge
     stl[MZ_S_SELECTS] += 1;
     stl[MZ_S_PATH_EDGES] += D;
@@ -650,6 +746,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
 // --------------------------------------------------------------------------------------------
 // One simulation step of one tree: [expand + back-propagate (sim s)] -> [select (sim s+1)] ->
 // [gather the selected leaf's parent hidden state].
+// Memory round trips: (1) tree header (scalar); (2) tables, path, node records, q, RNG window,
+// network outputs, statistics -- all issued before one wait; (3) value entries of the path
+// (chunk 0) and path-node scalars, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
 template <bool EB, bool SEL>
 __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
@@ -659,9 +758,36 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     const int l = threadIdx.x;
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
+    // ---- round 1 (independent of the tree state): tables, network outputs ----
+    if (SEL) {
+        for (int i = l; i < g.PS; i += kWave) glds4(d.pb + i, s.pb + (i - l));
+        for (int i = l; i < 2 * g.PS; i += kWave) glds4((const int *)d.sq + i, (int *)s.sq + (i - l));
+    }
+    float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
+    if (EB) {
+        for (int i = l; i < g.PS + 1; i += kWave) glds4(d.lp + i, s.lp + (i - l));
+        const size_t ib = (size_t)t * g.A;
+        if (l < g.A) {
+            pol = a.policy[ib + l];
+            bet = a.beta[ib + l];
+        }
+        r_in = a.reward[t];
+        v_in = a.value[t];
+    }
+    long long *st = d.stats + (size_t)t * MZ_S_COUNT;
+    long long st_old = (l < MZ_S_COUNT) ? st[l] : 0;
     TreeHdr h = d.hdr[t];
+    h.cursor = uni(h.cursor);
+    h.tot = uni(h.tot);
+    h.D = uni(h.D);
+    h.err = uni(h.err);
+    h.mm_cnt = uni(h.mm_cnt);
+    h.mm_min = unif(h.mm_min);
+    h.mm_max = unif(h.mm_max);
+    h.leaf = uni(h.leaf);
     stamp(ts, 1);
     if (h.err) {
+        wait_vm();  // no LDS-DMA may be outstanding when the wave ends
         if (SEL && l == 0) {
             a.idx_x[t] = 0;
             a.idy[t] = t;
@@ -674,51 +800,48 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
 #pragma unroll
     for (int k = 0; k < MZ_S_COUNT; ++k) stl[k] = 0;
 
-    // ---- round 1: tables, path, expansion inputs ----
-    // (LDS-DMA: lane l's element goes to base + 4*l, the base being uniform across the wave)
-    if (SEL) {
-        for (int i = l; i < g.PS; i += kWave) glds4(d.pb + i, s.pb + (i - l));
-        for (int i = l; i < 2 * g.PS; i += kWave) glds4((const int *)d.sq + i, (int *)s.sq + (i - l));
-    }
-    float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
-    if (EB) {
-        for (int i = l; i < g.PS + 1; i += kWave) glds4(d.lp + i, s.lp + (i - l));
+    // ---- round 2: path, node records, q, RNG window ----
+    const int tot = h.tot;
+    const size_t nb = (size_t)t * g.P;
+    if (EB)
         for (int i = l; i < 2 * (h.D + 1); i += kWave)
             glds4((const int *)(d.path + (size_t)t * g.PS) + i, (int *)s.path + (i - l));
-        const size_t ib = (size_t)t * g.A;
-        if (l < g.A) {
-            pol = a.policy[ib + l];
-            bet = a.beta[ib + l];
+    for (int i0 = 0; i0 < tot; i0 += kWave) {
+        if (i0 + l < tot) {
+            glds16(d.A + nb + i0 + l, s.A + i0);
+            glds16(d.Bn + nb + i0 + l, s.B + i0);
+            if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
         }
-        r_in = a.reward[t];
-        v_in = a.value[t];
     }
+    const int wbase = h.cursor;
+    for (int i0 = 0; i0 < kRngWin; i0 += kWave)
+        if (wbase + i0 + l < g.W) glds4(d.R + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
     wait_vm();
     stamp(ts, 2);
 
-    // ---- round 2: node records, q, path-node value scalars, RNG window ----
-    const int tot = h.tot;
-    const size_t nb = (size_t)t * g.P;
-    for (int i = l; i < ((tot + kWave - 1) / kWave) * kWave; i += kWave) {
-        if (i < tot) {
-            glds16(d.A + nb + i, s.A + (i - l));
-            glds16(d.Bn + nb + i, s.B + (i - l));
-            if (EB) glds4(d.Q + nb + i, s.Q + (i - l));
+    // ---- round 3: path-node scalars + chunk 0 of the value entries, in flight during expand ----
+    int cnt0 = 0, n0 = 0, nv0 = 0, off0 = 0;
+    if (EB) {
+        for (int i = l; i <= h.D; i += kWave) glds16(d.C + nb + s.path[i].x, s.C + (i - l));
+        cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, off0);
+    }
+    PucTables pt;
+    unsigned rw0 = 0, rw1 = 0;
+    if (SEL) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = r * kWave + l;
+            pt.pb[r] = (i < g.PS) ? s.pb[i] : 0.f;
+            pt.sq[r] = (i < g.PS) ? s.sq[i] : 0.0;
         }
     }
-    if (EB)
-        for (int i = l; i <= h.D; i += kWave) glds16(d.C + nb + s.path[i].x, s.C + (i - l));
-    const int wbase = h.cursor;
-    for (int i = l; i < kRngWin; i += kWave)
-        if (wbase + i < g.W) glds4(d.R + (size_t)t * g.W + wbase + i, s.rng + (i - l));
-    wait_vm();
     stamp(ts, 3);
 
     int cursor = h.cursor;
     int ntot = tot;
     if (EB) {
         // ---- CTree::expand_and_backprop (cnode.cpp:452-469) ----
-        const int leaf = s.path[h.D].x;
+        const int leaf = uni(s.path[h.D].x);
         long long st_new = 0;
         const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, cursor, ntot, s.rng, wbase, s.A, s.B, s.Q, err,
                                    st_new);
@@ -739,13 +862,17 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         if (!err) {
             h.cursor = cursor;
             h.tot = ntot;
-            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, err, stl, ts);
+            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, cnt0, n0, nv0, off0, err, stl, ts);
         }
     }
     stamp(ts, 6);
     if (SEL && !err) {
+        // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
+        int perr = 0;  // words past the stream end only matter if the walk consumes them
+        rw0 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
+        rw1 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + kWave + l, perr);
         int idx = 0, act = 0;
-        select_walk(g, d, s, t, a.discount, h, wbase, err, idx, act, stl);
+        select_walk(g, d, s, t, a.discount, h, wbase, rw0, rw1, pt, err, idx, act, stl);
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;
@@ -757,10 +884,11 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
             char *dst = a.gather_out + (long long)t * a.row_bytes;
             const long long rb = a.row_bytes;
             if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0) {
-                for (long long o = (long long)l * 16; o < rb; o += 16 * kWave)
-                    *(int4 *)(dst + o) = *(const int4 *)(src + o);
+                for (long long o2 = (long long)l * 16; o2 < rb; o2 += 16 * kWave)
+                    *(int4 *)(dst + o2) = *(const int4 *)(src + o2);
             } else {
-                for (long long o = (long long)l * 4; o < rb; o += 4 * kWave) *(int *)(dst + o) = *(const int *)(src + o);
+                for (long long o2 = (long long)l * 4; o2 < rb; o2 += 4 * kWave)
+                    *(int *)(dst + o2) = *(const int *)(src + o2);
             }
         }
     } else if (SEL && l == 0) {
@@ -776,19 +904,16 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     stamp(ts, 9);
     if (MZ_STAMPS && EB && SEL && !err) {
         // phases: header, stage1, stage2, expand, backup, minmax, select(+outputs), gather, epilogue
-        if (ts[4] == 0) ts[4] = ts[3];
-        if (ts[5] == 0) ts[5] = ts[4];
-        if (ts[6] == 0) ts[6] = ts[5];
-        if (ts[7] == 0) ts[7] = ts[6];
         for (int k = 0; k < 9; ++k) stl[MZ_S_CYC_HEADER + k] += (long long)(ts[k + 1] - ts[k]);
         stl[MZ_S_STAMPED] += 1;
     }
-    if (l == 0) {
-        long long *st = d.stats + (size_t)t * MZ_S_COUNT;
+    // per-tree statistics: lane k owns counter k
+    long long mine = 0;
 #pragma unroll
-        for (int k = 0; k < MZ_S_COUNT; ++k) st[k] += stl[k];
-        if (err) atomicOr(d.err, err);
-    }
+    for (int k = 0; k < MZ_S_COUNT; ++k)
+        if (l == k) mine = stl[k];
+    if (l < MZ_S_COUNT) st[l] = st_old + mine;
+    if (l == 0 && err) atomicOr(d.err, err);
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
@@ -818,8 +943,8 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
     const size_t nb = (size_t)t * g.P;
     const int4 ra = d.A[nb];
     const int4 rbn = d.Bn[nb];
-    const int nc = rbn.y & 0xffff;
-    const int fc = rbn.x;
+    const int nc = uni(rbn.y) & 0xffff;
+    const int fc = uni(rbn.x);
     float *fout = (float *)out;
     if (l == 0) {
         fout[t] = (nc > 0) ? i2f(ra.z) : 0.f;
