@@ -650,6 +650,13 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
     }
     long long scored = 0;
     while (true) {
+        // pin the loop-carried walk state to SGPRs (readfirstlane of a uniform value is free)
+        x = uni(x);
+        D = uni(D);
+        cursor = uni(cursor);
+        phsx = uni(phsx);
+        xa = uni4(xa);
+        xb = uni4(xb);
         const int nc = xb.y & 0xffff;
         if (nc == 0) break;
         const int fc = xb.x;
