@@ -87,7 +87,11 @@ enum mz_stat {
     MZ_S_CYC_GATHER = 16,    /* hidden-state gather                                        */
     MZ_S_CYC_EPILOGUE = 17,  /* header / path write-back                                   */
     MZ_S_STAMPED = 18,       /* stamped launches x trees                                   */
-    MZ_S_COUNT = 19
+    MZ_S_CYC_SEL_READ = 19,  /* selection levels: children records LDS read               */
+    MZ_S_CYC_SEL_SCORE = 20, /* selection levels: pUCT scores                              */
+    MZ_S_CYC_SEL_PICK = 21,  /* selection levels: arg-max scan, tie-break word             */
+    MZ_S_CYC_SEL_STEP = 22,  /* selection levels: descend                                  */
+    MZ_S_COUNT = 23
 };
 
 /* --- library -------------------------------------------------------------------------- */

@@ -48,6 +48,10 @@ STATS = [
     "cyc_gather",
     "cyc_epilogue",
     "stamped",
+    "cyc_sel_read",
+    "cyc_sel_score",
+    "cyc_sel_pick",
+    "cyc_sel_step",
 ]
 
 EXPORTS = [

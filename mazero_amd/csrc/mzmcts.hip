@@ -4,29 +4,31 @@
 //
 // Execution model.  One wavefront owns one tree for the whole kernel (grid = #trees, block = 64):
 // no cross-tree interaction exists in the algorithm (cnode.cpp:633-641, 663-669), so there is no
-// inter-workgroup communication at all.  Each launch stages the tree's hot node records from HBM
-// into LDS with LDS-DMA (global_load_lds), walks / updates the tree in LDS, and writes back only
-// the records it changed.  Per-simulation work is one launch (mz_expand_backup_select) fusing
-// expansion + back-propagation of simulation s with the selection of s+1 and the leaf
-// hidden-state gather that feeds the network.
+// inter-workgroup communication at all.  Each launch stages the tree's node records from HBM into
+// LDS with LDS-DMA (global_load_lds), walks / updates the tree in LDS, and writes back only what
+// it changed.  Per-simulation work is one launch (mz_expand_backup_select) fusing expansion +
+// back-propagation of simulation s with the selection of s+1 and the leaf hidden-state gather.
 //
 // Data layout in HBM (tree-major structure of arrays; node n of tree t at index t*P + n, where
 // P = K*(S+2) is the reference's per-root pool, cnode.cpp:562):
-//   A[t][n]  int4  {visit, prior, val, reward}           read for every scored child
-//   Bn[t][n] int4  {first_child, nc | action<<16, pred_value, hidden_state_index_x}
-//   C[t][n]  float4{weighted_sum, tot_weight, -, -}       SubTreeValueSet scalars (utils.h:29)
-//   D[t][n]  float4{pred_prob, beta, beta_hat, -}         readback-only
-//   Q[t][n]  float  q = qsa - parent.pred_value           member of the min/max set (cnode.cpp:435,445)
-//   V[t][n][E] int2 {depth, value}                        every backed-up value of the node, sorted by
-//                                                         (depth, value); E = S+1 = max visits
+//   A[t][n]  int4  {visit, prior, value, reward}           (value = ws/tw, 0 while unexpanded)
+//   Bn[t][n] int4  {first_child, nc | action<<8 | (maxdepth+1)<<16, pred_value, hidden_state_index_x}
+//   Q[t][n]  float q = qsa - parent.pred_value, the node's member of the min/max set (cnode.cpp:435,445)
+//   PP[t][n] float parent's pred_value (fixed when the node is created)
+//   C[t][n]  float4{weighted_sum, tot_weight, -, -}        SubTreeValueSet scalars (utils.h:29)
+//   D[t][n]  float4{pred_prob, beta, beta_hat, -}          readback-only
+//   V[t][n][E] int2 {depth, value}                         every backed-up value of the node, sorted by
+//                                                          (depth, value); E = S+1 = max visits
 //   R[t][W]  u32   the tree's pre-generated std::mt19937 stream (cnode.cpp:574)
 // Children of a node are contiguous (the reference allocates them consecutively, cnode.cpp:290-292),
-// so scoring a node's children is one coalesced 16-B-per-lane LDS read.
+// so scoring a node's children is one 16-B-per-lane LDS read.
 //
 // Bit-exactness.  Built with -ffp-contract=off, correctly rounded f32 division and no fast-math;
-// every float expression keeps the reference's operation order.  The pUCT log term uses a table
-// computed on the host with glibc logf (the reference calls logf, cnode.cpp:313), and sqrt(n) is
-// tabulated in double on the host too, so no device transcendental enters a result.
+// every float expression keeps the reference's operation order.  The pUCT coefficient
+// pb_c(n, v) = (float)((double)(logf((n + c2 + 1)/c2) + c1) * (sqrt(n) / (v + 1))) (cnode.cpp:313-314)
+// depends only on the parent's total child visits n and the child's visits v <= n; the host
+// tabulates it with glibc logf and IEEE double arithmetic, i.e. with exactly the reference's
+// operations, so no device transcendental enters a result.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -48,6 +50,7 @@ constexpr int kWave = 64;
 constexpr int kRngWin = 256;     // RNG words staged in LDS per launch
 constexpr int kMaxActions = 64;  // one lane per action
 constexpr int kMtN = 624;
+constexpr int kTableLdsMax = 48 * 1024;  // the pUCT table is staged in LDS when it fits this
 
 enum : int {
     kErrPool = 1,      // node pool exhausted (more expansions than simulation_num allows)
@@ -66,26 +69,30 @@ struct TreeHdr {
 
 struct Geo {
     int B, A, K, S, P, E, W, PS;
+    int TT;         // pUCT table entries (PS*(PS+1)/2, padded to 4)
+    int use_table;  // pUCT table staged in LDS (else pb/sq tables + double arithmetic)
     int root_offset;
     unsigned seed;
     float one_minus_rho, delta;
     int reg_cap;  // value entries staged in LDS per back-propagation chunk
     // dynamic-LDS byte offsets of k_step
-    int oA, oB, oQ, oC, oPath, oPb, oSq, oLp, oRng, oBoot, oReg, lds;
+    int oA, oB, oQ, oPP, oVs, oC, oPath, oFlag, oT, oPb, oSq, oLp, oRng, oBoot, oReg, lds;
 };
 
 struct Dev {
     int4 *A;
     int4 *Bn;
+    float *Q;
+    float *PP;
     float4 *C;
     float4 *D;
-    float *Q;
     int2 *V;
     unsigned *R;
     TreeHdr *hdr;
     int2 *path;  // [B][PS] {node, visit-at-selection}
     long long *stats;
     int *err;
+    float *T;    // [TT] pUCT coefficient table, index n*(n+1)/2 + v
     float *pb;   // [PS] logf((n + c2 + 1)/c2) + c1
     double *sq;  // [PS] sqrt(n)
     float *lp;   // [PS+1] lambda^d as a float chain
@@ -96,7 +103,6 @@ struct StepArgs {
     float discount;
     int K;
     const float *reward, *value, *policy, *beta;  // expansion inputs
-    float c2, c1;                                  // unused in-kernel (tables); kept for clarity
     int *idx_x, *idy, *act;
     const char *pool;
     long long pool_stride, row_bytes;
@@ -131,6 +137,12 @@ __device__ __forceinline__ double rld(double v, int l) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// Node-record field packing: Bn.y = nc | action<<8 | (maxdepth+1)<<16
+__device__ __forceinline__ int nc_of(int y) { return y & 0xff; }
+__device__ __forceinline__ int act_of(int y) { return (y >> 8) & 0xff; }
+__device__ __forceinline__ int md_of(int y) { return (int)((unsigned)y >> 16) - 1; }
+__device__ __forceinline__ int pack_y(int nc, int act, int md) { return nc | (act << 8) | ((md + 1) << 16); }
+
 // Wait for this wave's memory traffic (LDS-DMA included via vmcnt) / LDS traffic; compiler fence.
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -154,7 +166,8 @@ __device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
 }
 
 // Whole-wave reductions with DPP (no LDS round trips): xor-pairs, xor-quads, half-row and row
-// mirrors reduce each 16-lane row; the four row results are combined from SGPRs.
+// mirrors reduce each 16-lane row; the four row results are combined from SGPRs.  All lanes must
+// be active.
 template <int CTRL>
 __device__ __forceinline__ int dpp(int v) {
     return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xf, 0xf, false);
@@ -192,20 +205,21 @@ __device__ __forceinline__ int value_lim(int c, float one_minus_rho) {
 // --------------------------------------------------------------------------------------------
 struct Lds {
     int4 *A, *B;
-    float *Q;
+    float *Q, *PP, *Vs;
     float4 *C;
     int2 *path;
-    float *pb;
+    int *flag;
+    float *T, *pb;
     double *sq;
     float *lp;
     unsigned *rng;
     float *boot;
     int2 *reg;
     __device__ Lds(unsigned char *s, const Geo &g)
-        : A((int4 *)(s + g.oA)), B((int4 *)(s + g.oB)), Q((float *)(s + g.oQ)), C((float4 *)(s + g.oC)),
-          path((int2 *)(s + g.oPath)), pb((float *)(s + g.oPb)), sq((double *)(s + g.oSq)),
-          lp((float *)(s + g.oLp)), rng((unsigned *)(s + g.oRng)), boot((float *)(s + g.oBoot)),
-          reg((int2 *)(s + g.oReg)) {}
+        : A((int4 *)(s + g.oA)), B((int4 *)(s + g.oB)), Q((float *)(s + g.oQ)), PP((float *)(s + g.oPP)),
+          Vs((float *)(s + g.oVs)), C((float4 *)(s + g.oC)), path((int2 *)(s + g.oPath)), flag((int *)(s + g.oFlag)),
+          T((float *)(s + g.oT)), pb((float *)(s + g.oPb)), sq((double *)(s + g.oSq)), lp((float *)(s + g.oLp)),
+          rng((unsigned *)(s + g.oRng)), boot((float *)(s + g.oBoot)), reg((int2 *)(s + g.oReg)) {}
 };
 
 // RNG word `idx` (per lane) of tree t: LDS window [wbase, wbase+kRngWin) or HBM.
@@ -228,11 +242,11 @@ __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, co
 // 2656-2713, 3348-3378): double prefix sums of beta/sum(beta), last forced to 1.0; two engine words
 // per draw; index = lower_bound.  Fewer than two actions => no draw and no engine word.
 // Creates the children in HBM (and in the LDS mirrors when given), advances cursor / tot and
-// returns nc.
+// returns nc.  `pv` is the expanded node's pred_value (the children's PP).
 // --------------------------------------------------------------------------------------------
-__device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float bet, float noi, float eps, int K,
-                           int &cursor, int &tot, const unsigned *win, int wbase, int4 *sA, int4 *sB, float *sQ,
-                           int &err, long long &st_new) {
+__device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float bet, float noi, float eps, int K, float pv,
+                           int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
+                           long long &st_new) {
     const int l = lane_id();
     const int A = g.A;
     int cnt = 0;  // number of draws that hit action l
@@ -281,17 +295,19 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
         float prior = (eps > 0) ? (pol * (1 - eps) + noi * eps) : pol;
         prior = prior * bh / bet;  // prior * betahat_prob / beta_prob
         const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
-        const int4 b4 = make_int4(0, (l << 16), f2i(0.0f), -1);
+        const int4 b4 = make_int4(0, pack_y(0, l, -1), f2i(0.0f), -1);
         const size_t gi = (size_t)t * g.P + c;
         d.A[gi] = a4;
         d.Bn[gi] = b4;
         d.C[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
         d.D[gi] = make_float4(pol, bet, bh, 0.f);
         d.Q[gi] = 0.f;
-        if (sA) {
-            sA[c] = a4;
-            sB[c] = b4;
-            sQ[c] = 0.f;
+        d.PP[gi] = pv;
+        if (s) {
+            s->A[c] = a4;
+            s->B[c] = b4;
+            s->Q[c] = 0.f;
+            s->PP[c] = pv;
         }
     }
     st_new += nc;
@@ -376,8 +392,7 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
     int err = 0;
     int cursor = 0, tot = 1;
     long long st_new = 0;
-    const int nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, cursor, tot, w0, 0, nullptr, nullptr, nullptr, err,
-                               st_new);
+    const int nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new);
     if (l == 0) {
         // root: CNode(1,1,1,1,true) (cnode.cpp:217), expanded, visit += 1, subtree.update(value, 0)
         const size_t gi = (size_t)t * g.P;
@@ -389,10 +404,11 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
         ws += lp0 * v;
         const float val = (nc > 0) ? ws / tw : 0.f;
         d.A[gi] = make_int4(1, f2i(1.0f), f2i(val), f2i(r));
-        d.Bn[gi] = make_int4(1, nc | (0 << 16), f2i(v), 0);
+        d.Bn[gi] = make_int4(1, pack_y(nc, 0, 0), f2i(v), 0);
         d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
         d.D[gi] = make_float4(1.f, 1.f, 1.f, 0.f);
         d.Q[gi] = 0.f;
+        d.PP[gi] = 0.f;
         d.V[gi * g.E] = make_int2(0, f2i(v));
         TreeHdr h;
         h.cursor = cursor;
@@ -413,25 +429,31 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
 }
 
 // --------------------------------------------------------------------------------------------
-// Back-propagation staging: the value entries of path nodes [i0, i0+cnt) -> LDS with LDS-DMA.
-// Chunks hold <= 64 nodes whose entries fit g.reg_cap.  Returns cnt (uniform); lane l gets its
-// node id, entry count (= visit at selection) and entry offset inside the staging area.
+// Back-propagation staging: the value entries of the path nodes [i0, i0+cnt) that need them ->
+// LDS with LDS-DMA.  A node needs its entries only when the new value's depth is not beyond its
+// deepest entry (otherwise the update is an append with an empty depth class: always so in K=1
+// chains).  Chunks hold <= 64 nodes whose needed entries fit g.reg_cap.  Returns cnt (uniform);
+// lane l gets its node id, entry count (= visit at selection), need flag and staging offset.
 // --------------------------------------------------------------------------------------------
-__device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &off) {
+__device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &need,
+                             int &off) {
     const int l = lane_id();
     const int i = i0 + l;
     n = 0;
     nv = 0;
+    need = 0;
     off = 0;
     if (i <= D) {
         const int2 pe = s.path[i];
         n = pe.x;
         nv = pe.y;
+        need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
     }
     const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
+    const int cost = need ? nv : 0;
     int acc = 0, cnt = 0;
     for (int j = 0; j < lim; ++j) {  // uniform prefix sum over the chunk
-        const int vj = rl(nv, j);
+        const int vj = rl(cost, j);
         if (acc + vj > g.reg_cap) break;
         if (l == j) off = acc;
         acc += vj;
@@ -439,7 +461,9 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
     }
     const int2 *gV = d.V + (size_t)t * g.P * g.E;
     int *regdw = (int *)s.reg;
-    for (int j = 0; j < cnt; ++j) {
+    const unsigned long long nm = ballot(l < cnt && need);
+    for (unsigned long long m = nm; m; m &= m - 1ull) {
+        const int j = __builtin_ctzll(m);
         const int nj = rl(n, j), vj = rl(nv, j), oj = rl(off, j);
         const int dw = 2 * vj;
         const int *src = (const int *)(gV + (size_t)nj * g.E);
@@ -459,7 +483,8 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
 // multiset's content.  Chunk 0's entries must already be in flight (stage_regions).
 // --------------------------------------------------------------------------------------------
 __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float disc, TreeHdr &h,
-                       int cnt0, int n0, int nv0, int off0, int &err, long long *stl, unsigned long long *ts) {
+                       int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl,
+                       unsigned long long *ts) {
     const int l = lane_id();
     // bootstrap values (cnode.cpp:424,448)
     {
@@ -479,7 +504,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         }
     }
     int2 *gV = d.V + (size_t)t * g.P * g.E;
-    int cnt = cnt0, n = n0, nv = nv0, off = off0;
+    int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0;
     long long ent_r = 0, ent_w = 0;
     for (int i0 = 0; i0 <= D;) {
         if (cnt == 0) {
@@ -494,8 +519,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             const float key = s.boot[i];
             const int2 *R = s.reg + off;
             int lo = nv, c = 0, pv = 0;
-            // entries are sorted by depth: a new deepest depth (always so in K=1 chains) needs no scan
-            if (nv > 0 && R[nv - 1].x >= dep) {
+            if (need) {
                 lo = 0;
                 int j = 0;
                 for (; j + 4 <= nv; j += 4) {
@@ -554,23 +578,29 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             ent_w += nv - pos + 1;
             // node scalars
             const int4 a4 = s.A[n];
-            const int nc = s.B[n].y & 0xffff;
+            const int4 b4 = s.B[n];
+            const int nc = nc_of(b4.y);
             const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
             const int4 na = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
+            const int md = md_of(b4.y);
             s.A[n] = na;
             const size_t gi = (size_t)t * g.P + n;
             d.A[gi] = na;
             d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
+            if (dep > md) {
+                const int4 nb4 = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
+                s.B[n] = nb4;
+                d.Bn[gi] = nb4;
+            }
             if (i >= 1) {
-                const float ppv = i2f(s.B[s.path[i - 1].x].z);
-                const float q = (i2f(a4.w) + disc * val) - ppv;  // get_qsa - father->pred_value
+                const float q = (i2f(a4.w) + disc * val) - s.PP[n];  // get_qsa - father->pred_value
                 s.Q[n] = q;
                 d.Q[gi] = q;
             }
         }
         wait_lds();
         i0 += cnt;
-        if (i0 <= D) cnt = stage_regions(g, d, s, t, D, i0, n, nv, off);
+        if (i0 <= D) cnt = stage_regions(g, d, s, t, D, i0, n, nv, need, off);
     }
     stl[MZ_S_BACKUP_NODES] += D + 1;
     stl[MZ_S_ENTRIES_READ] += ent_r;
@@ -594,53 +624,20 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
     stl[MZ_S_MINMAX_NODES] += tot - 1;
 }
 
-// pUCT table entry n (uniform): lanes hold entries l, 64+l, 128+l, 192+l; larger n from LDS.
-struct PucTables {
-    float pb[4];
-    double sq[4];
-};
-__device__ __forceinline__ void puct_lookup(const PucTables &pt, const Lds &s, int n, float &pb, double &sq) {
-    const int r = n >> 6, o = n & 63;
-    if (r == 0) {
-        pb = rlf(pt.pb[0], o);
-        sq = rld(pt.sq[0], o);
-    } else if (r == 1) {
-        pb = rlf(pt.pb[1], o);
-        sq = rld(pt.sq[1], o);
-    } else if (r == 2) {
-        pb = rlf(pt.pb[2], o);
-        sq = rld(pt.sq[2], o);
-    } else if (r == 3) {
-        pb = rlf(pt.pb[3], o);
-        sq = rld(pt.sq[3], o);
-    } else {
-        pb = unif(s.pb[n]);
-        const double q = s.sq[n];
-        const long long qb = __double_as_longlong(q);
-        sq = __longlong_as_double(((long long)(unsigned)uni((int)(qb >> 32)) << 32) |
-                                  (unsigned)uni((int)(qb & 0xffffffffll)));
-    }
+// pUCT coefficient pb_c(n, v) for this lane (cnode.cpp:313-314): the host-built table when it is
+// staged, else the same double arithmetic on the pb / sq tables.
+__device__ __forceinline__ float puct(const Geo &g, const Lds &s, int n, int v) {
+    if (g.use_table) return s.T[n * (n + 1) / 2 + v];
+    const float pbl = s.pb[n];
+    const double sqn = s.sq[n];
+    return (float)((double)pbl * (sqn / (double)(v + 1)));
 }
 
-// --------------------------------------------------------------------------------------------
-// CTree::select_path (cnode.cpp:381-413) with select_child (337-379) and ucb_score (297-335),
-// walking the LDS copy.  Lane j scores child j; the arg-max with epsilon ties is the reference's
-// sequential scan over the lanes (uniform loop), one engine word when the tie list is non-empty.
-// All walk state is wave-uniform (SGPRs).  RNG words come from two registers holding the window
-// [wbase, wbase+128) (lane j: words j and 64+j), then the LDS window, then HBM.
-// --------------------------------------------------------------------------------------------
-__device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float disc, TreeHdr &h, int lds_base,
-                            unsigned rw0, unsigned rw1, const PucTables &pt, int &err, int &out_idx, int &out_act,
-                            long long *stl) {
-    const int wbase = h.cursor;  // register window [wbase, wbase + 128)
+// value part of ucb_score for every node (cnode.cpp:317-331): qsa - parent.pred_value (0 while
+// unvisited), min/max normalised, clamped to [0, 1].  One float division per node, all nodes in
+// parallel, so the walk itself only multiplies and adds.
+__device__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const TreeHdr &h) {
     const int l = lane_id();
-    int x = 0;
-    int4 xa = uni4(s.A[0]);
-    int4 xb = uni4(s.B[0]);
-    int phsx = xb.w;  // hidden_state_index_x of the current node's parent
-    int D = 0;
-    int cursor = h.cursor;
-    if (l == 0) s.path[0] = make_int2(0, xa.x);
     const bool mm_on = h.mm_cnt > 0;
     const float mmn = h.mm_min, mmx = h.mm_max;
     float den = 0.f;
@@ -648,99 +645,200 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
         const float delta = mmx - mmn;
         den = (g.delta < delta) ? delta : g.delta;  // std::max(delta_lb, delta)
     }
-    long long scored = 0;
-    while (true) {
-        // pin the loop-carried walk state to SGPRs (readfirstlane of a uniform value is free)
-        x = uni(x);
-        D = uni(D);
-        cursor = uni(cursor);
-        phsx = uni(phsx);
-        xa = uni4(xa);
-        xb = uni4(xb);
-        const int nc = xb.y & 0xffff;
-        if (nc == 0) break;
-        const int fc = xb.x;
-        // every lane reads its child's records (one LDS round trip per level)
-        const bool has = l < nc;
-        int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
-        if (has) {
-            ca = s.A[fc + l];
-            cb = s.B[fc + l];
+    for (int base = 0; base < tot; base += kWave) {
+        const int n = base + l;
+        if (n < tot) {
+            const int4 a4 = s.A[n];
+            float vs = (a4.x == 0) ? 0.0f : ((i2f(a4.w) + disc * i2f(a4.z)) - s.PP[n]);
+            if (mm_on) vs = (vs - mmn) / den;
+            if (vs < 0) vs = 0;
+            if (vs > 1) vs = 1;
+            s.Vs[n] = vs;
         }
-        int ci = 0;
-        if (x == 0 && xa.x <= nc) {
-            ci = xa.x - 1;  // forced root round-robin (cnode.cpp:398-399)
-        } else {
-            const int ntot = xa.x - 1;  // total_children_visit_counts = node->visit_count - 1
-            if (ntot < 0 || ntot >= g.PS) {
-                err |= kErrTable;
+    }
+    wait_lds();
+}
+
+__device__ __forceinline__ unsigned select_word(const Geo &g, const Dev &d, const Lds &s, int t, int cursor, int wbase,
+                                                int lds_base, unsigned rw0, unsigned rw1, int &err) {
+    const int o = cursor - wbase;
+    if (o >= 0 && o < kWave) return (unsigned)rl((int)rw0, o);
+    if (o >= kWave && o < 2 * kWave) return (unsigned)rl((int)rw1, o - kWave);
+    if (cursor - lds_base >= 0 && cursor - lds_base < kRngWin) return (unsigned)uni((int)s.rng[cursor - lds_base]);
+    if (cursor < g.W) return (unsigned)uni((int)d.R[(size_t)t * g.W + cursor]);
+    err |= kErrRng;
+    return 0u;
+}
+
+// ucb score of node `child` under node `parent` (used for the single-child checks)
+__device__ __forceinline__ float path_score(const Geo &g, const Lds &s, int parent, int child, int &err) {
+    const int n = s.A[parent].x - 1;
+    if (n < 0 || n >= g.PS) {
+        err |= kErrTable;
+        return 0.f;
+    }
+    const int4 ca = s.A[child];
+    return puct(g, s, n, ca.x) * i2f(ca.y) + s.Vs[child];
+}
+
+// --------------------------------------------------------------------------------------------
+// CTree::select_path (cnode.cpp:381-413) with select_child (337-379) and ucb_score (297-335).
+//
+// K = 1 trees are chains (one child per expansion), so the path is every node in creation order
+// and the only data-dependent effect of a level is whether select_child's tie list is non-empty
+// (score >= FLOAT_MIN, not NaN), which decides whether an engine word is consumed: all levels
+// are scored in parallel and the words counted with one ballot.
+//
+// Otherwise the walk goes level by level in LDS.  Lane j scores child j; the sequential arg-max
+// with epsilon ties (list = [r] + {i > r : s_i >= M - eps}, M the max and r its first index)
+// becomes a DPP max and two ballots; one engine word when the list is non-empty.  A single-child
+// level takes child 0 whatever the score, so it is walked speculatively (one word assumed) and
+// its score checked in parallel afterwards; a failed check re-walks exactly.
+// --------------------------------------------------------------------------------------------
+__device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base,
+                            unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl) {
+    const int l = lane_id();
+    const int cursor0 = h.cursor;
+    const int wbase = cursor0;  // register window [wbase, wbase + 128)
+    long long scored = 0;
+    if (g.K == 1) {
+        const int D = tot - 1;
+        if (D < 1) err |= kErrRoot;
+        if (D + 1 > g.PS) err |= kErrPath;
+        int words = 0;
+        if (!err) {
+            const int root_visit = uni(s.A[0].x);
+            for (int base = 0; base <= D; base += kWave) {
+                const int i = base + l;
+                bool valid = false;
+                if (i <= D) {
+                    s.path[i] = make_int2(i, s.A[i].x);
+                    if (i >= 1 && !(i == 1 && root_visit <= 1)) {
+                        const float sc = path_score(g, s, i - 1, i, err);
+                        valid = sc >= -1000000.0f;  // tie list non-empty (FLOAT_MIN, utils.h:12)
+                    }
+                }
+                words += __popcll(ballot(valid));
+            }
+            scored = D;
+        }
+        h.cursor = cursor0 + words;
+        h.D = D;
+        h.leaf = D;
+        const int4 pb = uni4(s.B[D > 0 ? D - 1 : 0]);
+        const int4 lb = uni4(s.B[D > 0 ? D : 0]);
+        out_idx = pb.w;
+        out_act = act_of(lb.y);
+        stl[MZ_S_SELECTS] += 1;
+        stl[MZ_S_PATH_EDGES] += D;
+        stl[MZ_S_SCORED] += scored;
+        wait_lds();
+        int2 *gp = d.path + (size_t)t * g.PS;
+        for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
+        return;
+    }
+
+    int x = 0, D = 0, cursor = cursor0, phsx = 0;
+    int4 xa = make_int4(0, 0, 0, 0), xb = xa;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        const bool spec = (attempt == 0);
+        x = 0;
+        D = 0;
+        cursor = cursor0;
+        xa = uni4(s.A[0]);
+        xb = uni4(s.B[0]);
+        phsx = xb.w;
+        scored = 0;
+        if (l == 0) {
+            s.path[0] = make_int2(0, xa.x);
+            s.flag[0] = 0;
+        }
+        while (true) {
+            x = uni(x);
+            D = uni(D);
+            cursor = uni(cursor);
+            xa = uni4(xa);
+            xb = uni4(xb);
+            const int nc = nc_of(xb.y);
+            if (nc == 0) break;
+            const int fc = xb.x;
+            const bool has = l < nc;
+            int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
+            float vsl = 0.f;
+            if (has) {
+                ca = s.A[fc + l];
+                cb = s.B[fc + l];
+                vsl = s.Vs[fc + l];
+            }
+            int ci = 0, fl = 0;
+            if (x == 0 && xa.x <= nc) {
+                ci = xa.x - 1;  // forced root round-robin (cnode.cpp:398-399)
+            } else if (nc == 1 && spec) {
+                ++cursor;  // select_child of a single child: child 0, one word if its score is valid
+                fl = 1;
+            } else {
+                const int ntot = xa.x - 1;  // total_children_visit_counts = node->visit_count - 1
+                if (ntot < 0 || ntot >= g.PS) {
+                    err |= kErrTable;
+                    break;
+                }
+                float sc = -INFINITY;
+                if (has) sc = puct(g, s, ntot, ca.x) * i2f(ca.y) + vsl;
+                scored += nc;
+                const float M = wave_max(sc);
+                unsigned long long lst;
+                if (M > -1000000.0f) {
+                    const unsigned long long first = ballot(has && sc == M);
+                    const int r = __builtin_ctzll(first);
+                    lst = ballot(has && sc >= M - 0.000001f) & (~0ull << r);
+                } else {
+                    lst = ballot(has && sc >= -1000000.0f);
+                }
+                const int cnt = __popcll(lst);
+                if (cnt > 0) {
+                    const unsigned w = select_word(g, d, s, t, cursor, wbase, lds_base, rw0, rw1, err);
+                    ++cursor;
+                    int k = (cnt == 1) ? 0 : (int)(w % (unsigned)cnt);  // gen() % max_index_lst.size()
+                    for (; k > 0; --k) lst &= lst - 1ull;
+                    ci = __builtin_ctzll(lst);
+                }
+            }
+            // descend
+            phsx = xb.w;
+            x = fc + ci;
+            xa = make_int4(rl(ca.x, ci), rl(ca.y, ci), rl(ca.z, ci), rl(ca.w, ci));
+            xb = make_int4(rl(cb.x, ci), rl(cb.y, ci), rl(cb.z, ci), rl(cb.w, ci));
+            if (D + 1 >= g.PS) {
+                err |= kErrPath;
                 break;
             }
-            float pbl;
-            double sqn;
-            puct_lookup(pt, s, ntot, pbl, sqn);
-            const float ppv = i2f(xb.z);
-            float score = 0.f;
-            if (has) {
-                const int v = ca.x;
-                float pbc = pbl;
-                pbc = (float)((double)pbc * (sqn / (double)(v + 1)));
-                const float prior_score = pbc * i2f(ca.y);
-                float vs = (v == 0) ? 0.0f : ((i2f(ca.w) + disc * i2f(ca.z)) - ppv);
-                if (mm_on) vs = (vs - mmn) / den;
-                if (vs < 0) vs = 0;
-                if (vs > 1) vs = 1;
-                score = prior_score + vs;
-            }
-            scored += nc;
-            float maxs = -1000000.0f;  // FLOAT_MIN (utils.h:12)
-            unsigned long long lst = 0ull;
-            for (int j = 0; j < nc; ++j) {
-                const float sj = rlf(score, j);
-                if (maxs < sj) {
-                    maxs = sj;
-                    lst = 1ull << j;
-                } else if (sj >= maxs - 0.000001f) {
-                    lst |= 1ull << j;
-                }
-            }
-            const int cnt = __popcll(lst);
-            if (cnt > 0) {
-                const int o = cursor - wbase;
-                unsigned w;
-                if (o >= 0 && o < kWave) w = (unsigned)rl((int)rw0, o);
-                else if (o >= kWave && o < 2 * kWave) w = (unsigned)rl((int)rw1, o - kWave);
-                else if (cursor - lds_base >= 0 && cursor - lds_base < kRngWin)
-                    w = (unsigned)uni((int)s.rng[cursor - lds_base]);
-                else if (cursor < g.W) w = (unsigned)uni((int)d.R[(size_t)t * g.W + cursor]);
-                else {
-                    err |= kErrRng;
-                    w = 0u;
-                }
-                ++cursor;
-                int k = (cnt == 1) ? 0 : (int)(w % (unsigned)cnt);  // gen() % max_index_lst.size()
-                for (; k > 0; --k) lst &= lst - 1ull;
-                ci = __builtin_ctzll(lst);
+            ++D;
+            if (l == 0) {
+                s.path[D] = make_int2(x, xa.x);
+                s.flag[D] = fl;
             }
         }
-        // descend
-        phsx = xb.w;
-        x = fc + ci;
-        xa = make_int4(rl(ca.x, ci), rl(ca.y, ci), rl(ca.z, ci), rl(ca.w, ci));
-        xb = make_int4(rl(cb.x, ci), rl(cb.y, ci), rl(cb.z, ci), rl(cb.w, ci));
-        if (D + 1 >= g.PS) {
-            err |= kErrPath;
-            break;
+        if (!spec) break;
+        // verify the speculated single-child levels in parallel
+        wait_lds();
+        bool bad = false;
+        for (int base = 1; base <= D; base += kWave) {
+            const int i = base + l;
+            bool b = false;
+            if (i <= D && s.flag[i]) {
+                const float sc = path_score(g, s, s.path[i - 1].x, s.path[i].x, err);
+                b = !(sc >= -1000000.0f);
+            }
+            bad = bad || (ballot(b) != 0ull);
         }
-        ++D;
-        if (l == 0) s.path[D] = make_int2(x, xa.x);
+        if (!bad) break;
     }
     if (D == 0) err |= kErrRoot;
     h.cursor = cursor;
     h.D = D;
     h.leaf = x;
-    out_idx = phsx;        // parent->hidden_state_index_x
-    out_act = xb.y >> 16;  // children_action of the last edge
+    out_idx = phsx;          // parent->hidden_state_index_x
+    out_act = act_of(xb.y);  // children_action of the last edge
     stl[MZ_S_SELECTS] += 1;
     stl[MZ_S_PATH_EDGES] += D;
     stl[MZ_S_SCORED] += scored;
@@ -753,9 +851,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, float dis
 // --------------------------------------------------------------------------------------------
 // One simulation step of one tree: [expand + back-propagate (sim s)] -> [select (sim s+1)] ->
 // [gather the selected leaf's parent hidden state].
-// Memory round trips: (1) tree header (scalar); (2) tables, path, node records, q, RNG window,
-// network outputs, statistics -- all issued before one wait; (3) value entries of the path
-// (chunk 0) and path-node scalars, in flight while the leaf is expanded.
+// Memory round trips: (1) tree header (scalar), tables and network outputs; (2) path, node
+// records, q / parent values, RNG window -- issued before one wait; (3) path-node scalars and the
+// value entries the back-propagation needs, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
 template <bool EB, bool SEL>
 __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
@@ -767,12 +865,20 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     stamp(ts, 0);
     // ---- round 1 (independent of the tree state): tables, network outputs ----
     if (SEL) {
-        for (int i = l; i < g.PS; i += kWave) glds4(d.pb + i, s.pb + (i - l));
-        for (int i = l; i < 2 * g.PS; i += kWave) glds4((const int *)d.sq + i, (int *)s.sq + (i - l));
+        if (g.use_table) {
+            for (int i0 = 0; i0 < g.TT; i0 += 4 * kWave)
+                if (i0 + 4 * l < g.TT) glds16(d.T + i0 + 4 * l, s.T + i0);
+        } else {
+            for (int i0 = 0; i0 < g.PS; i0 += kWave)
+                if (i0 + l < g.PS) glds4(d.pb + i0 + l, s.pb + i0);
+            for (int i0 = 0; i0 < 2 * g.PS; i0 += kWave)
+                if (i0 + l < 2 * g.PS) glds4((const int *)d.sq + i0 + l, (int *)s.sq + i0);
+        }
     }
     float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
     if (EB) {
-        for (int i = l; i < g.PS + 1; i += kWave) glds4(d.lp + i, s.lp + (i - l));
+        for (int i0 = 0; i0 < g.PS + 1; i0 += kWave)
+            if (i0 + l < g.PS + 1) glds4(d.lp + i0 + l, s.lp + i0);
         const size_t ib = (size_t)t * g.A;
         if (l < g.A) {
             pol = a.policy[ib + l];
@@ -782,7 +888,7 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         v_in = a.value[t];
     }
     long long *st = d.stats + (size_t)t * MZ_S_COUNT;
-    long long st_old = (l < MZ_S_COUNT) ? st[l] : 0;
+    const long long st_old = (l < MZ_S_COUNT) ? st[l] : 0;
     TreeHdr h = d.hdr[t];
     h.cursor = uni(h.cursor);
     h.tot = uni(h.tot);
@@ -807,16 +913,17 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
 #pragma unroll
     for (int k = 0; k < MZ_S_COUNT; ++k) stl[k] = 0;
 
-    // ---- round 2: path, node records, q, RNG window ----
+    // ---- round 2: path, node records, q / parent values, RNG window ----
     const int tot = h.tot;
     const size_t nb = (size_t)t * g.P;
     if (EB)
-        for (int i = l; i < 2 * (h.D + 1); i += kWave)
-            glds4((const int *)(d.path + (size_t)t * g.PS) + i, (int *)s.path + (i - l));
+        for (int i0 = 0; i0 < 2 * (h.D + 1); i0 += kWave)
+            if (i0 + l < 2 * (h.D + 1)) glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
     for (int i0 = 0; i0 < tot; i0 += kWave) {
         if (i0 + l < tot) {
             glds16(d.A + nb + i0 + l, s.A + i0);
             glds16(d.Bn + nb + i0 + l, s.B + i0);
+            glds4(d.PP + nb + i0 + l, s.PP + i0);
             if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
         }
     }
@@ -826,21 +933,12 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     wait_vm();
     stamp(ts, 2);
 
-    // ---- round 3: path-node scalars + chunk 0 of the value entries, in flight during expand ----
-    int cnt0 = 0, n0 = 0, nv0 = 0, off0 = 0;
+    // ---- round 3: path-node scalars + the value entries back-propagation needs (chunk 0) ----
+    int cnt0 = 0, n0 = 0, nv0 = 0, need0 = 0, off0 = 0;
     if (EB) {
-        for (int i = l; i <= h.D; i += kWave) glds16(d.C + nb + s.path[i].x, s.C + (i - l));
-        cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, off0);
-    }
-    PucTables pt;
-    unsigned rw0 = 0, rw1 = 0;
-    if (SEL) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = r * kWave + l;
-            pt.pb[r] = (i < g.PS) ? s.pb[i] : 0.f;
-            pt.sq[r] = (i < g.PS) ? s.sq[i] : 0.0;
-        }
+        for (int i0 = 0; i0 <= h.D; i0 += kWave)
+            if (i0 + l <= h.D) glds16(d.C + nb + s.path[i0 + l].x, s.C + i0);
+        cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
     }
     stamp(ts, 3);
 
@@ -850,15 +948,14 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         // ---- CTree::expand_and_backprop (cnode.cpp:452-469) ----
         const int leaf = uni(s.path[h.D].x);
         long long st_new = 0;
-        const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, cursor, ntot, s.rng, wbase, s.A, s.B, s.Q, err,
-                                   st_new);
+        const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new);
         stl[MZ_S_EXPANDS] += 1;
         stl[MZ_S_NEW_CHILDREN] += st_new;
         if (!err && l == 0) {
             const int4 la = s.A[leaf];
             const int4 lb = s.B[leaf];
             const int4 na = make_int4(la.x, la.y, la.z, f2i(r_in));
-            const int4 nbv = make_int4(tot, nc | (lb.y & 0xffff0000), f2i(v_in), a.hsx);
+            const int4 nbv = make_int4(tot, pack_y(nc, act_of(lb.y), md_of(lb.y)), f2i(v_in), a.hsx);
             s.A[leaf] = na;
             s.B[leaf] = nbv;
             d.A[nb + leaf] = na;
@@ -869,17 +966,18 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         if (!err) {
             h.cursor = cursor;
             h.tot = ntot;
-            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, cnt0, n0, nv0, off0, err, stl, ts);
+            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl, ts);
         }
     }
     stamp(ts, 6);
     if (SEL && !err) {
+        value_scores(g, s, h.tot, a.discount, h);
         // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
         int perr = 0;  // words past the stream end only matter if the walk consumes them
-        rw0 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
-        rw1 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + kWave + l, perr);
+        const unsigned rw0 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
+        const unsigned rw1 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + kWave + l, perr);
         int idx = 0, act = 0;
-        select_walk(g, d, s, t, a.discount, h, wbase, rw0, rw1, pt, err, idx, act, stl);
+        select_walk(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl);
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;
@@ -950,7 +1048,7 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
     const size_t nb = (size_t)t * g.P;
     const int4 ra = d.A[nb];
     const int4 rbn = d.Bn[nb];
-    const int nc = uni(rbn.y) & 0xffff;
+    const int nc = nc_of(uni(rbn.y));
     const int fc = uni(rbn.x);
     float *fout = (float *)out;
     if (l == 0) {
@@ -965,7 +1063,7 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
         cb = d.Bn[nb + fc + l];
         cd = d.D[nb + fc + l];
     }
-    const int act = cb.y >> 16;
+    const int act = act_of(cb.y);
     // marginal visit counts / priors: lane a collects the child whose action is a
     int mv = 0;
     float mp = 0.f;
@@ -1081,6 +1179,16 @@ int ensure_tables(mz_batch *b, float c2, float c1) {
         pb[n] = ::logf(x) + c1;
         sq[n] = ::sqrt((double)n);
     }
+    // pb_c(n, v) for every parent total n and child visits v <= n, with ucb_score's operations:
+    // pb_c = pb[n]; pb_c *= (sqrt(n) / (v + 1))   (float *= double)
+    std::vector<float> T(b->geo.TT, 0.f);
+    for (int n = 0; n < b->PS; ++n)
+        for (int v = 0; v <= n; ++v) {
+            float pbc = pb[n];
+            pbc = (float)((double)pbc * (sq[n] / (double)(v + 1)));
+            T[(size_t)n * (n + 1) / 2 + v] = pbc;
+        }
+    HIP_TRY(hipMemcpyAsync(b->dev.T, T.data(), sizeof(float) * T.size(), hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipMemcpyAsync(b->dev.pb, pb.data(), sizeof(float) * b->PS, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipMemcpyAsync(b->dev.sq, sq.data(), sizeof(double) * b->PS, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
@@ -1157,6 +1265,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
                     "agent_num != 1: the per-agent sequential search of this fork builds 1-agent trees "
                     "(mcts_sampled.py:53,89); joint-action trees are not implemented on the GPU yet");
     if (A > kMaxActions) return fail(MZ_ERR_UNSUPPORTED, "action_space_size > 64");
+    if (S > 65000) return fail(MZ_ERR_UNSUPPORTED, "simulation_num > 65000");
     if (K > 4096) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 4096");
     auto *b = new mz_batch;
     b->B = B;
@@ -1199,12 +1308,18 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         if (cap < S + 1) cap = S + 1;
         g.reg_cap = (int)cap;
     }
+    g.TT = ((g.PS * (g.PS + 1) / 2) + 3) & ~3;
+    g.use_table = (4 * g.TT <= kTableLdsMax) ? 1 : 0;
     int o = 0;
     g.oA = o; o += round16(16 * g.P);
     g.oB = o; o += round16(16 * g.P);
     g.oQ = o; o += round16(4 * g.P);
+    g.oPP = o; o += round16(4 * g.P);
+    g.oVs = o; o += round16(4 * g.P);
     g.oC = o; o += round16(16 * g.PS);
     g.oPath = o; o += round16(8 * g.PS);
+    g.oFlag = o; o += round16(4 * g.PS);
+    g.oT = o; o += g.use_table ? round16(4 * g.TT) : 0;
     g.oPb = o; o += round16(4 * (g.PS + kWave));
     g.oSq = o; o += round16(8 * (g.PS + kWave));
     g.oLp = o; o += round16(4 * (g.PS + 1 + kWave));
@@ -1224,6 +1339,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     rc |= dalloc(b, &d.C, nodes);
     rc |= dalloc(b, &d.D, nodes);
     rc |= dalloc(b, &d.Q, nodes);
+    rc |= dalloc(b, &d.PP, nodes);
+    rc |= dalloc(b, &d.T, (size_t)g.TT + 4 * kWave);
     rc |= dalloc(b, &d.V, nodes * b->E);
     rc |= dalloc(b, &d.R, (size_t)B * b->W);
     rc |= dalloc(b, &d.hdr, (size_t)B);
@@ -1333,8 +1450,6 @@ int mz_select(mz_batch *b, float c2, float c1, float discount, int32_t *idx_x, i
     if (rc) return rc;
     StepArgs a{};
     a.discount = discount;
-    a.c2 = c2;
-    a.c1 = c1;
     if (mem == MZ_MEM_HOST) {
         a.idx_x = b->sel_dev;
         a.idy = b->sel_dev + b->B;
@@ -1420,8 +1535,6 @@ int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const f
     a.hsx = hsx;
     a.discount = discount;
     a.K = K;
-    a.c2 = c2;
-    a.c1 = c1;
     rc = expand_inputs(b, rewards, values, policy, beta, MZ_MEM_DEVICE, a);
     if (rc) return rc;
     a.idx_x = idx_x;
