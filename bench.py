@@ -207,8 +207,11 @@ def main():
         frac_fused = (S - 1) / (S + 1)
         bytes_fused = (sel_b + exp_b + bak_b) * frac_fused + gat_b
         bytes_per_launch = bytes_fused / launches_fused
+        # Keep the GPU busy while the host enqueues the instrumented search, so that the event
+        # pairs bracket back-to-back kernel executions rather than host submission gaps.
         evs = []
         with torch.cuda.stream(stream):
+            torch.cuda._sleep(int(2e8))  # ~0.1 s of GPU spinning
             for sd in searches:
                 one_search(sd, timed_events=evs)
         torch.cuda.synchronize()
@@ -232,6 +235,7 @@ def main():
             roofline["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
             roofline["select_level_cycles"] = {k[8:]: round(st[k] / max(1, st["path_edges"]), 1)
                                                for k in st if k.startswith("cyc_sel_")}
+            roofline["phase_cycles"] = {k: v for k, v in roofline["phase_cycles"].items() if not k.startswith("sel_")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -91,7 +91,13 @@ enum mz_stat {
     MZ_S_CYC_SEL_SCORE = 20, /* selection levels: pUCT scores                              */
     MZ_S_CYC_SEL_PICK = 21,  /* selection levels: arg-max scan, tie-break word             */
     MZ_S_CYC_SEL_STEP = 22,  /* selection levels: descend                                  */
-    MZ_S_COUNT = 23
+    MZ_S_CYC_EXP_CDF = 23,   /* expansion: sampling distribution                           */
+    MZ_S_CYC_EXP_DRAW = 24,  /* expansion: K draws                                         */
+    MZ_S_CYC_EXP_NODES = 25, /* expansion: child creation                                  */
+    MZ_S_CYC_BAK_BOOT = 26,  /* back-propagation: bootstrap values                         */
+    MZ_S_CYC_BAK_WAIT = 27,  /* back-propagation: waiting for staged entries               */
+    MZ_S_CYC_BAK_NODES = 28, /* back-propagation: node updates                             */
+    MZ_S_COUNT = 29
 };
 
 /* --- library -------------------------------------------------------------------------- */

@@ -52,6 +52,12 @@ STATS = [
     "cyc_sel_score",
     "cyc_sel_pick",
     "cyc_sel_step",
+    "cyc_exp_cdf",
+    "cyc_exp_draw",
+    "cyc_exp_nodes",
+    "cyc_bak_boot",
+    "cyc_bak_wait",
+    "cyc_bak_nodes",
 ]
 
 EXPORTS = [

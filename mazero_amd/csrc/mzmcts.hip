@@ -51,6 +51,7 @@ constexpr int kRngWin = 256;     // RNG words staged in LDS per launch
 constexpr int kMaxActions = 64;  // one lane per action
 constexpr int kMtN = 624;
 constexpr int kTableLdsMax = 48 * 1024;  // the pUCT table is staged in LDS when it fits this
+constexpr int kNxt = 32;  // RNG words for the next expansion carried in the tree header (2K <= kNxt)
 
 enum : int {
     kErrPool = 1,      // node pool exhausted (more expansions than simulation_num allows)
@@ -65,6 +66,7 @@ struct TreeHdr {
     int cursor, tot, D, err;
     float mm_min, mm_max;
     int mm_cnt, leaf;
+    unsigned nxt[kNxt];  // R[cursor .. cursor + kNxt): the next expansion's engine words
 };
 
 struct Geo {
@@ -102,6 +104,7 @@ struct StepArgs {
     int hsx;
     float discount;
     int K;
+    int ne, pe;  // host bounds on the node count and path length (skip waiting for the header)
     const float *reward, *value, *policy, *beta;  // expansion inputs
     int *idx_x, *idy, *act;
     const char *pool;
@@ -246,10 +249,12 @@ __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, co
 // --------------------------------------------------------------------------------------------
 __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float bet, float noi, float eps, int K, float pv,
                            int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
-                           long long &st_new) {
+                           long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl) {
     const int l = lane_id();
     const int A = g.A;
     int cnt = 0;  // number of draws that hit action l
+    unsigned long long e0 = 0, e1 = 0, e2 = 0;
+    if (MZ_STAMPS && stl) e0 = __builtin_amdgcn_s_memtime();
     if (A < 2) {
         cnt = (l == 0) ? K : 0;
     } else {
@@ -265,14 +270,19 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
             if (l == a) cp = acc;
         }
         if (l == A - 1) cp = 1.0;
+        if (MZ_STAMPS && stl) {
+            asm volatile("" ::"v"(cp));
+            e1 = __builtin_amdgcn_s_memtime();
+        }
         // K draws, 64 at a time; lane k of a chunk performs draw k0+k
         for (int k0 = 0; k0 < K; k0 += kWave) {
             const int nk = (K - k0) < kWave ? (K - k0) : kWave;
             int idx = 0;
             if (l < nk) {
                 const int w = cursor + 2 * (k0 + l);
-                const double w1 = (double)rng_word_lane(g, d, win, wbase, t, w, err);
-                const double w2 = (double)rng_word_lane(g, d, win, wbase, t, w + 1, err);
+                const bool reg = have_w && k0 == 0;
+                const double w1 = (double)(reg ? w1r : rng_word_lane(g, d, win, wbase, t, w, err));
+                const double w2 = (double)(reg ? w2r : rng_word_lane(g, d, win, wbase, t, w + 1, err));
                 double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
                 if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
                 for (int a = 0; a < A; ++a) idx += (rld(cp, a) < u) ? 1 : 0;
@@ -280,6 +290,11 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
             for (int k = 0; k < nk; ++k) cnt += (rl(idx, k) == l) ? 1 : 0;
         }
         cursor += 2 * K;
+    }
+    if (MZ_STAMPS && stl) {
+        asm volatile("" ::"v"(cnt));
+        e2 = __builtin_amdgcn_s_memtime();
+        if (e1 == 0) e1 = e0;
     }
     const bool has = (l < A) && cnt > 0;
     const unsigned long long m = ballot(has);
@@ -312,6 +327,13 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
     }
     st_new += nc;
     tot += nc;  // the children occupy [old tot, old tot + nc)
+    if (MZ_STAMPS && stl) {
+        wait_lds();
+        const unsigned long long e3 = __builtin_amdgcn_s_memtime();
+        stl[MZ_S_CYC_EXP_CDF] += (long long)(e1 - e0);
+        stl[MZ_S_CYC_EXP_DRAW] += (long long)(e2 - e1);
+        stl[MZ_S_CYC_EXP_NODES] += (long long)(e3 - e2);
+    }
     return nc;
 }
 
@@ -392,7 +414,8 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
     int err = 0;
     int cursor = 0, tot = 1;
     long long st_new = 0;
-    const int nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new);
+    const int nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false,
+                               0u, 0u, nullptr);
     if (l == 0) {
         // root: CNode(1,1,1,1,true) (cnode.cpp:217), expanded, visit += 1, subtree.update(value, 0)
         const size_t gi = (size_t)t * g.P;
@@ -419,6 +442,7 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
         h.mm_max = 0.f;
         h.mm_cnt = 0;
         h.leaf = 0;
+        for (int j = 0; j < kNxt; ++j) h.nxt[j] = (cursor + j < kMtN) ? w0[cursor + j] : 0u;
         d.hdr[t] = h;
         d.path[(size_t)t * g.PS] = make_int2(0, 1);
         long long *st = d.stats + (size_t)t * MZ_S_COUNT;
@@ -450,14 +474,18 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
         need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
     }
     const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
-    const int cost = need ? nv : 0;
-    int acc = 0, cnt = 0;
-    for (int j = 0; j < lim; ++j) {  // uniform prefix sum over the chunk
-        const int vj = rl(cost, j);
-        if (acc + vj > g.reg_cap) break;
+    // prefix sum of the needed entry counts over the chunk: a uniform loop over the needing lanes
+    // only (none in K=1 chains); the chunk ends before the first node that would overflow reg_cap
+    int acc = 0, cnt = lim;
+    for (unsigned long long m = ballot(l < lim && need); m; m &= m - 1ull) {
+        const int j = __builtin_ctzll(m);
+        const int vj = rl(nv, j);
+        if (acc + vj > g.reg_cap) {
+            cnt = j;
+            break;
+        }
         if (l == j) off = acc;
         acc += vj;
-        ++cnt;
     }
     const int2 *gV = d.V + (size_t)t * g.P * g.E;
     int *regdw = (int *)s.reg;
@@ -486,6 +514,8 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
                        int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl,
                        unsigned long long *ts) {
     const int l = lane_id();
+    const unsigned long long b0 = (MZ_STAMPS != 0) ? __builtin_amdgcn_s_memtime() : 0ull;
+    unsigned long long b1 = 0, bw = 0;
     // bootstrap values (cnode.cpp:424,448)
     {
         float b = value;
@@ -503,6 +533,10 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             if (l < n) s.boot[base - l - 1] = mine;
         }
     }
+    if (MZ_STAMPS) {
+        wait_lds();
+        b1 = __builtin_amdgcn_s_memtime();
+    }
     int2 *gV = d.V + (size_t)t * g.P * g.E;
     int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0;
     long long ent_r = 0, ent_w = 0;
@@ -511,8 +545,11 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             err |= kErrPath;
             return;
         }
+        unsigned long long w0s = 0;
+        if (MZ_STAMPS) w0s = __builtin_amdgcn_s_memtime();
         wait_vm();
         wait_lds();
+        if (MZ_STAMPS) bw += __builtin_amdgcn_s_memtime() - w0s;
         const int i = i0 + l;
         if (l < cnt) {
             const int dep = D - i;
@@ -605,6 +642,13 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
     stl[MZ_S_BACKUP_NODES] += D + 1;
     stl[MZ_S_ENTRIES_READ] += ent_r;
     stl[MZ_S_ENTRIES_WRITTEN] += ent_w;
+    if (MZ_STAMPS) {
+        wait_lds();
+        const unsigned long long b2 = __builtin_amdgcn_s_memtime();
+        stl[MZ_S_CYC_BAK_BOOT] += (long long)(b1 - b0);
+        stl[MZ_S_CYC_BAK_WAIT] += (long long)bw;
+        stl[MZ_S_CYC_BAK_NODES] += (long long)(b2 - b1 - bw);
+    }
     stamp(ts, 5);
     // min/max over the q of visited non-root nodes
     float mn = INFINITY, mx = -INFINITY;
@@ -863,7 +907,10 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     const int l = threadIdx.x;
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
-    // ---- round 1 (independent of the tree state): tables, network outputs ----
+    const size_t nb = (size_t)t * g.P;
+    // ---- round 1: everything that does not depend on the tree header, issued together with it:
+    // tables, network outputs, the expansion's engine words (carried in the header), statistics,
+    // and the node records / path within the host's bounds a.ne / a.pe ----
     if (SEL) {
         if (g.use_table) {
             for (int i0 = 0; i0 < g.TT; i0 += 4 * kWave)
@@ -875,10 +922,22 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
                 if (i0 + l < 2 * g.PS) glds4((const int *)d.sq + i0 + l, (int *)s.sq + i0);
         }
     }
+    for (int i0 = 0; i0 < a.ne; i0 += kWave) {
+        if (i0 + l < a.ne) {
+            glds16(d.A + nb + i0 + l, s.A + i0);
+            glds16(d.Bn + nb + i0 + l, s.B + i0);
+            glds4(d.PP + nb + i0 + l, s.PP + i0);
+            if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
+        }
+    }
     float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
+    unsigned w1r = 0u, w2r = 0u;
+    const bool have_w = 2 * a.K <= kNxt;
     if (EB) {
         for (int i0 = 0; i0 < g.PS + 1; i0 += kWave)
             if (i0 + l < g.PS + 1) glds4(d.lp + i0 + l, s.lp + i0);
+        for (int i0 = 0; i0 < 2 * a.pe; i0 += kWave)
+            if (i0 + l < 2 * a.pe) glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
         const size_t ib = (size_t)t * g.A;
         if (l < g.A) {
             pol = a.policy[ib + l];
@@ -886,21 +945,28 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         }
         r_in = a.reward[t];
         v_in = a.value[t];
+        if (have_w && l < a.K) {
+            w1r = d.hdr[t].nxt[2 * l];
+            w2r = d.hdr[t].nxt[2 * l + 1];
+        }
     }
     long long *st = d.stats + (size_t)t * MZ_S_COUNT;
     const long long st_old = (l < MZ_S_COUNT) ? st[l] : 0;
-    TreeHdr h = d.hdr[t];
-    h.cursor = uni(h.cursor);
-    h.tot = uni(h.tot);
-    h.D = uni(h.D);
-    h.err = uni(h.err);
-    h.mm_cnt = uni(h.mm_cnt);
-    h.mm_min = unif(h.mm_min);
-    h.mm_max = unif(h.mm_max);
-    h.leaf = uni(h.leaf);
+    TreeHdr h;
+    {
+        const TreeHdr *hp = d.hdr + t;
+        h.cursor = uni(hp->cursor);
+        h.tot = uni(hp->tot);
+        h.D = uni(hp->D);
+        h.err = uni(hp->err);
+        h.mm_cnt = uni(hp->mm_cnt);
+        h.mm_min = unif(hp->mm_min);
+        h.mm_max = unif(hp->mm_max);
+        h.leaf = uni(hp->leaf);
+    }
+    wait_vm();
     stamp(ts, 1);
     if (h.err) {
-        wait_vm();  // no LDS-DMA may be outstanding when the wave ends
         if (SEL && l == 0) {
             a.idx_x[t] = 0;
             a.idy[t] = t;
@@ -913,33 +979,37 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
 #pragma unroll
     for (int k = 0; k < MZ_S_COUNT; ++k) stl[k] = 0;
 
-    // ---- round 2: path, node records, q / parent values, RNG window ----
     const int tot = h.tot;
-    const size_t nb = (size_t)t * g.P;
-    if (EB)
-        for (int i0 = 0; i0 < 2 * (h.D + 1); i0 += kWave)
-            if (i0 + l < 2 * (h.D + 1)) glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
-    for (int i0 = 0; i0 < tot; i0 += kWave) {
-        if (i0 + l < tot) {
-            glds16(d.A + nb + i0 + l, s.A + i0);
-            glds16(d.Bn + nb + i0 + l, s.B + i0);
-            glds4(d.PP + nb + i0 + l, s.PP + i0);
-            if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
+    // slow path: the host bounds were too small (e.g. a graph replayed out of sequence)
+    if (tot > a.ne || (EB && h.D + 1 > a.pe)) {
+        for (int i0 = a.ne; i0 < tot; i0 += kWave) {
+            if (i0 + l < tot) {
+                glds16(d.A + nb + i0 + l, s.A + i0);
+                glds16(d.Bn + nb + i0 + l, s.B + i0);
+                glds4(d.PP + nb + i0 + l, s.PP + i0);
+                if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
+            }
         }
+        if (EB)
+            for (int i0 = 2 * a.pe; i0 < 2 * (h.D + 1); i0 += kWave)
+                if (i0 + l < 2 * (h.D + 1))
+                    glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
+        wait_vm();
     }
-    const int wbase = h.cursor;
-    for (int i0 = 0; i0 < kRngWin; i0 += kWave)
-        if (wbase + i0 + l < g.W) glds4(d.R + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
-    wait_vm();
     stamp(ts, 2);
 
-    // ---- round 3: path-node scalars + the value entries back-propagation needs (chunk 0) ----
+    // ---- round 2 (asynchronous): path-node scalars, the value entries back-propagation needs,
+    // the RNG window -- in flight while the leaf is expanded ----
     int cnt0 = 0, n0 = 0, nv0 = 0, need0 = 0, off0 = 0;
     if (EB) {
         for (int i0 = 0; i0 <= h.D; i0 += kWave)
             if (i0 + l <= h.D) glds16(d.C + nb + s.path[i0 + l].x, s.C + i0);
         cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
     }
+    const int wbase = h.cursor;
+    for (int i0 = 0; i0 < kRngWin; i0 += kWave)
+        if (wbase + i0 + l < g.W) glds4(d.R + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
+    if (!EB || !have_w) wait_vm();  // the expansion reads its words from the window
     stamp(ts, 3);
 
     int cursor = h.cursor;
@@ -948,7 +1018,8 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         // ---- CTree::expand_and_backprop (cnode.cpp:452-469) ----
         const int leaf = uni(s.path[h.D].x);
         long long st_new = 0;
-        const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new);
+        const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new,
+                                   have_w, w1r, w2r, stl);
         stl[MZ_S_EXPANDS] += 1;
         stl[MZ_S_NEW_CHILDREN] += st_new;
         if (!err && l == 0) {
@@ -969,6 +1040,7 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
             backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl, ts);
         }
     }
+    wait_vm();  // RNG window (and anything staged) has landed
     stamp(ts, 6);
     if (SEL && !err) {
         value_scores(g, s, h.tot, a.discount, h);
@@ -1002,9 +1074,21 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
         a.act[t] = 0;
     }
     stamp(ts, 8);
-    if (l == 0) {
-        h.err = err;
-        d.hdr[t] = h;
+    // header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
+    {
+        int perr = 0;
+        TreeHdr *hp = d.hdr + t;
+        if (l < kNxt) hp->nxt[l] = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
+        if (l == 0) {
+            hp->cursor = h.cursor;
+            hp->tot = h.tot;
+            hp->D = h.D;
+            hp->err = err;
+            hp->mm_min = h.mm_min;
+            hp->mm_max = h.mm_max;
+            hp->mm_cnt = h.mm_cnt;
+            hp->leaf = h.leaf;
+        }
     }
     stamp(ts, 9);
     if (MZ_STAMPS && EB && SEL && !err) {
@@ -1121,6 +1205,7 @@ struct mz_batch {
     float rb_disc = 0.f;
     float tbl_c2 = NAN, tbl_c1 = NAN;
     bool prepared = false;
+    long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
 };
 
 namespace {
@@ -1206,8 +1291,16 @@ int dalloc(mz_batch *b, T **p, size_t count) {
     return MZ_OK;
 }
 
-int launch_step(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
+int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
+    // tot <= 1 + K * expansions and depth <= expansions: the kernel stages that much without
+    // waiting for the tree header (and falls back to the header's values if they are larger)
+    {
+        const long long ne = 1 + (long long)g.K * b->expansions;
+        a.ne = (int)(ne < g.P ? ne : g.P);
+        const long long pe = b->expansions + 1;
+        a.pe = (int)(pe < g.PS ? pe : g.PS);
+    }
     if (eb && sel)
         hipLaunchKernelGGL((k_step<true, true>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
     else if (eb)
@@ -1215,7 +1308,10 @@ int launch_step(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
     else
         hipLaunchKernelGGL((k_step<false, true>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
     HIP_TRY(hipGetLastError());
-    if (eb) b->rb_valid = b->rb_dev_valid = false;
+    if (eb) {
+        b->rb_valid = b->rb_dev_valid = false;
+        ++b->expansions;
+    }
     return MZ_OK;
 }
 
@@ -1436,6 +1532,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     HIP_TRY(hipGetLastError());
     b->rb_valid = b->rb_dev_valid = false;
     b->prepared = true;
+    b->expansions = 1;
     if (mem == MZ_MEM_HOST) return check_device_errors(b);
     return MZ_OK;
 }

@@ -231,3 +231,52 @@ def test_too_many_simulations_raise(gpu_lib):
         for s in range(10):
             tb.batch_selection(19652.0, 1.25, 0.997)
             tb.batch_expansion_and_backup(s + 1, 0.997, K, z, z, p, p)
+
+
+def test_graph_of_one_step_replayed(gpu_lib, port_lib):
+    """A HIP graph holding ONE fused simulation step, replayed for every simulation.  The host's
+    staging bounds baked into the graph are stale from the second replay on, so the kernel must
+    detect it from the tree header and stage the rest (slow path) -- results stay bit-exact."""
+    from mazero_amd.synthetic import DEFAULTS, make_search_inputs, readbacks
+
+    B, A, K, S = 48, 9, 5, 24
+    inp = make_search_inputs(np.random.default_rng(21), B, A, S)
+    c2, c1, g = DEFAULTS["pb_c_base"], DEFAULTS["pb_c_init"], DEFAULTS["discount"]
+    # CPU port with the same call sequence (hidden_state_index_x frozen at 1 like the graph)
+    ref = make_tb(port_lib, inp, K, {})
+    ref.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps, inp.root_noise)
+    ref_sel = [ref.batch_selection(c2, c1, g)[0]]
+    for s in range(S - 1):
+        ref.batch_expansion_and_backup(1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+        ref_sel.append(ref.batch_selection(c2, c1, g)[0])
+    dinp = to_device(inp)
+    tb = make_tb(gpu_lib, inp, K, {})
+    dev = torch.device("cuda")
+    out = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev),
+           torch.empty(B, 1, dtype=torch.int32, device=dev))
+    stat = [torch.empty_like(dinp.reward[0]), torch.empty_like(dinp.value[0]), torch.empty_like(dinp.policy[0]),
+            torch.empty_like(dinp.beta[0])]
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        tb.prepare(dinp.root_reward, dinp.root_value, dinp.root_policy, dinp.root_beta, K, dinp.noise_eps,
+                   dinp.root_noise)
+        tb.batch_selection_device(c2, c1, g, out=out)
+    torch.cuda.synchronize()
+    got = [out[0].cpu().tolist()]
+    graph = torch.cuda.CUDAGraph()
+    for st_, src in zip(stat, (dinp.reward[0], dinp.value[0], dinp.policy[0], dinp.beta[0])):
+        st_.copy_(src)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph, stream=stream):
+        tb.expansion_backup_selection_device(1, g, K, *stat, c2, c1, out=out)
+    # capture does not execute: replay the step for every simulation with fresh inputs
+    for s in range(S - 1):
+        for st_, src in zip(stat, (dinp.reward[s], dinp.value[s], dinp.policy[s], dinp.beta[s])):
+            st_.copy_(src)
+        graph.replay()
+        torch.cuda.synchronize()
+        got.append(out[0].cpu().tolist())
+    assert got == ref_sel
+    a, b = readbacks(tb, g), readbacks(ref, g)
+    for k in ("root_values", "marginal_visit_count", "sampled_qvalues"):
+        assert np.array_equal(a[k], b[k]), k
