@@ -261,9 +261,11 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
         // cumulative distribution (param_type::_M_initialize): sequential double sums
         const double bd = (l < A) ? (double)bet : 0.0;
         double sum = 0.0;
+#pragma unroll 8
         for (int a = 0; a < A; ++a) sum += rld(bd, a);
         const double p = bd / sum;
         double acc = 0.0, cp = 0.0;
+#pragma unroll 8
         for (int a = 0; a < A; ++a) {
             const double pa = rld(p, a);
             acc = (a == 0) ? pa : acc + pa;
@@ -274,20 +276,25 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
             asm volatile("" ::"v"(cp));
             e1 = __builtin_amdgcn_s_memtime();
         }
-        // K draws, 64 at a time; lane k of a chunk performs draw k0+k
+        // K draws, 64 at a time: lane k of a chunk forms the canonical double of draw k0+k; then,
+        // draw by draw, lane a compares its cp[a] with u and lower_bound = popcount of the ballot
         for (int k0 = 0; k0 < K; k0 += kWave) {
             const int nk = (K - k0) < kWave ? (K - k0) : kWave;
-            int idx = 0;
+            double u = 0.0;
             if (l < nk) {
                 const int w = cursor + 2 * (k0 + l);
                 const bool reg = have_w && k0 == 0;
                 const double w1 = (double)(reg ? w1r : rng_word_lane(g, d, win, wbase, t, w, err));
                 const double w2 = (double)(reg ? w2r : rng_word_lane(g, d, win, wbase, t, w + 1, err));
-                double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
+                u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
                 if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
-                for (int a = 0; a < A; ++a) idx += (rld(cp, a) < u) ? 1 : 0;
             }
-            for (int k = 0; k < nk; ++k) cnt += (rl(idx, k) == l) ? 1 : 0;
+#pragma unroll 4
+            for (int k = 0; k < nk; ++k) {
+                const double uk = rld(u, k);
+                const int idx = __popcll(ballot(l < A && cp < uk));
+                cnt += (l == idx) ? 1 : 0;
+            }
         }
         cursor += 2 * K;
     }
@@ -525,6 +532,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             const float r = (i >= 1) ? i2f(s.A[s.path[i].x].w) : 0.f;
             const int n = base < kWave ? base : kWave;
             float mine = 0.f;
+#pragma unroll 8
             for (int k = 0; k < n; ++k) {
                 const float rk = rlf(r, k);
                 b = rk + disc * b;
@@ -1014,6 +1022,10 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
 
     int cursor = h.cursor;
     int ntot = tot;
+    bool gath_pending = false;
+    int4 gv[4];
+    char *gdst = nullptr;
+    long long grb = 0;
     if (EB) {
         // ---- CTree::expand_and_backprop (cnode.cpp:452-469) ----
         const int leaf = uni(s.path[h.D].x);
@@ -1060,7 +1072,20 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
             const char *src = a.pool + (long long)idx * a.pool_stride + (long long)t * a.row_bytes;
             char *dst = a.gather_out + (long long)t * a.row_bytes;
             const long long rb = a.row_bytes;
-            if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0) {
+            if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0 && rb <= 4 * 16 * kWave) {
+                // up to 4 KiB per row: all loads in flight at once, stores after the header write-back
+                int4 v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const long long o2 = (long long)(k * kWave + l) * 16;
+                    if (o2 < rb) v[k] = *(const int4 *)(src + o2);
+                }
+                gath_pending = true;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) gv[k] = v[k];
+                gdst = dst;
+                grb = rb;
+            } else if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0) {
                 for (long long o2 = (long long)l * 16; o2 < rb; o2 += 16 * kWave)
                     *(int4 *)(dst + o2) = *(const int4 *)(src + o2);
             } else {
@@ -1088,6 +1113,13 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
             hp->mm_max = h.mm_max;
             hp->mm_cnt = h.mm_cnt;
             hp->leaf = h.leaf;
+        }
+    }
+    if (gath_pending) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const long long o2 = (long long)(k * kWave + l) * 16;
+            if (o2 < grb) *(int4 *)(gdst + o2) = gv[k];
         }
     }
     stamp(ts, 9);
