@@ -259,17 +259,29 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
         cnt = (l == 0) ? K : 0;
     } else {
         // cumulative distribution (param_type::_M_initialize): sequential double sums
+        // (serial chains, in blocks of 8 fully unrolled steps: readlane is convergent, so the
+        // compiler cannot unroll a runtime-count loop over it by itself)
         const double bd = (l < A) ? (double)bet : 0.0;
         double sum = 0.0;
-#pragma unroll 8
-        for (int a = 0; a < A; ++a) sum += rld(bd, a);
+        int a0 = 0;
+        for (; a0 + 8 <= A; a0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sum += rld(bd, a0 + j);
+        }
+        for (; a0 < A; ++a0) sum += rld(bd, a0);
         const double p = bd / sum;
-        double acc = 0.0, cp = 0.0;
-#pragma unroll 8
-        for (int a = 0; a < A; ++a) {
-            const double pa = rld(p, a);
-            acc = (a == 0) ? pa : acc + pa;
-            if (l == a) cp = acc;
+        double acc = rld(p, 0), cp = (l == 0) ? acc : 0.0;
+        a0 = 1;
+        for (; a0 + 8 <= A; a0 += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                acc = acc + rld(p, a0 + j);
+                cp = (l == a0 + j) ? acc : cp;
+            }
+        }
+        for (; a0 < A; ++a0) {
+            acc = acc + rld(p, a0);
+            cp = (l == a0) ? acc : cp;
         }
         if (l == A - 1) cp = 1.0;
         if (MZ_STAMPS && stl) {
@@ -289,7 +301,6 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
                 u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
                 if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
             }
-#pragma unroll 4
             for (int k = 0; k < nk; ++k) {
                 const double uk = rld(u, k);
                 const int idx = __popcll(ballot(l < A && cp < uk));
@@ -532,11 +543,17 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             const float r = (i >= 1) ? i2f(s.A[s.path[i].x].w) : 0.f;
             const int n = base < kWave ? base : kWave;
             float mine = 0.f;
-#pragma unroll 8
-            for (int k = 0; k < n; ++k) {
-                const float rk = rlf(r, k);
-                b = rk + disc * b;
-                if (l == k) mine = b;
+            int k = 0;
+            for (; k + 8 <= n; k += 8) {  // blocks of 8 fully unrolled steps (see expand_node)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    b = rlf(r, k + j) + disc * b;
+                    mine = (l == k + j) ? b : mine;
+                }
+            }
+            for (; k < n; ++k) {
+                b = rlf(r, k) + disc * b;
+                mine = (l == k) ? b : mine;
             }
             if (l < n) s.boot[base - l - 1] = mine;
         }
