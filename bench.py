@@ -20,8 +20,10 @@ torch.distributed (RCCL).
 
 Also reported (rank 0, N=1 only):
   roofline      dominant kernel k_step<true,true> (fused simulation step): algorithmic bytes per
-                launch (SURVEY §8d formula over the kernel's own counters) / its average duration
-                measured with HIP events on the launch stream in an instrumented eager pass
+                launch (SURVEY §8d formula over the kernel's own counters) / its average duration,
+                measured with HIP events on the launch stream around a graph of one search's 49
+                back-to-back fused launches; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per launch
+                from profiles/pmc_latest.json (scripts/pmc_summary.py) for the same workload
   cpu_baseline  the reference C++ ctree (oracle/_ref/libmzref.so, compiled from the reference
                 sources) -- or the CPU port when that is absent -- on the same synthetic inputs,
                 one host core, timing only the tree calls, over a bounded sample (~10 s)
@@ -48,7 +50,7 @@ CONFIGS = {  # name: (agents N, actions A) -- smac_maps.py:17-133, n_actions = 6
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -62,7 +64,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--seed", type=int, default=0)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def main():
@@ -192,7 +194,7 @@ def main():
     value = sims_per_rank * world / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
-    # ---- roofline of the dominant kernel (instrumented eager pass, rank 0) ----
+    # ---- roofline of the dominant kernel (rank 0) ----
     roofline = None
     if rank == 0:
         st = {k: sum(s1[k] - s0[k] for s0, s1 in zip(stats0, stats1)) for k in stats1[0]}
@@ -207,16 +209,37 @@ def main():
         frac_fused = (S - 1) / (S + 1)
         bytes_fused = (sel_b + exp_b + bak_b) * frac_fused + gat_b
         bytes_per_launch = bytes_fused / launches_fused
-        # Keep the GPU busy while the host enqueues the instrumented search, so that the event
-        # pairs bracket back-to-back kernel executions rather than host submission gaps.
-        evs = []
+        # Average duration of the fused kernel, measured with HIP events on the launch stream: a
+        # graph holding one search's S-1 fused launches (back to back, as in the timed region) is
+        # replayed after an eager prepare + first selection; (e1 - e0) / (S - 1) per replay.
+        sd0 = searches[0]
+        tb0 = sd0["tb"]
+        out0 = (sd0["idx"], sd0["idy"], sd0["act"])
+        steps_graph = torch.cuda.CUDAGraph()
         with torch.cuda.stream(stream):
-            torch.cuda._sleep(int(2e8))  # ~0.1 s of GPU spinning
-            for sd in searches:
-                one_search(sd, timed_events=evs)
+            tb0.prepare(sd0["rr"], sd0["rv"], sd0["rp"], sd0["rb"], K, sd0["eps"], sd0["rn"])
+            tb0.batch_selection_device(c2, c1, g, out=out0)
         torch.cuda.synchronize()
-        durs = [a.elapsed_time(b) * 1e-3 for a, b in evs]
-        avg = float(np.mean(durs))
+        with torch.cuda.graph(steps_graph, stream=stream):
+            for s in range(S - 1):
+                tb0.expansion_backup_selection_device(s + 1, g, K, sd0["r"][s], sd0["v"][s], sd0["p"][s], sd0["b"][s],
+                                                      c2, c1, out=out0, pool=sd0["pool"], gather_out=sd0["leaf"])
+        durs = []
+        with torch.cuda.stream(stream):
+            for rep in range(6):
+                tb0.prepare(sd0["rr"], sd0["rv"], sd0["rp"], sd0["rb"], K, sd0["eps"], sd0["rn"])
+                tb0.batch_selection_device(c2, c1, g, out=out0)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                steps_graph.replay()
+                e1.record()
+                e1.synchronize()
+                if rep > 0:
+                    durs.append(e0.elapsed_time(e1) * 1e-3 / (S - 1))
+        torch.cuda.synchronize()
+        tb0.synchronize()
+        avg = float(np.median(durs))
         achieved = bytes_per_launch / avg / 1e9
         roofline = dict(
             kernel="k_step<true,true> (fused expand+backup+select+gather)",
@@ -225,7 +248,7 @@ def main():
             peak=8000.0,
             unit="GB/s",
             frac=round(achieved / 8000.0, 6),
-            traffic=None,
+            traffic=pmc_traffic(args),
             bytes_per_launch=round(bytes_per_launch, 1),
             avg_launch_us=round(avg * 1e6, 3),
             mean_path_len=round(st["path_edges"] / max(1, st["selects"]), 3),
@@ -275,6 +298,27 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def workload_key(args):
+    return f"{args.map}:B{args.roots}:S{args.sims}:K{args.sampled_times}"
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of the fused kernel from the committed rocprofv3 PMC summary of the same
+    workload (profiles/pmc_latest.json, written by scripts/pmc_summary.py from separate
+    FETCH_SIZE and WRITE_SIZE passes), or None when there is none for this configuration."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None
+    key = workload_key(args)
+    ent = pm.get("workloads", {}).get(key)
+    if not ent:
+        return None
+    return ent.get("fused_bytes_per_launch")
 
 
 def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):

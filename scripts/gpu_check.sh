@@ -25,6 +25,7 @@ for s in $STEPS; do
     stamps) MZ_STAMPS=1 step bench_stamps 600 python bench.py --no-cpu ${BENCH_ARGS} ;;
     prof)   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --no-cpu --steps 10 ${BENCH_ARGS} ;;
     pmc)    step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o bench -- python3 "$R/bench.py" --no-cpu --steps 5 ${BENCH_ARGS} &&
-            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o bench -- python3 "$R/bench.py" --no-cpu --steps 5 ${BENCH_ARGS} ;;
+            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o bench -- python3 "$R/bench.py" --no-cpu --steps 5 ${BENCH_ARGS} &&
+            step pmc_summary 120 python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write --bench-args "${BENCH_ARGS}" --out gpurun_out/pmc_latest.json ;;
   esac
 done
