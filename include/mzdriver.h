@@ -1,0 +1,60 @@
+/*
+ * mzdriver.h — C-ABI of the device-side glue of the sampled-MCTS driver loop.
+ *
+ * The reference driver SampledMCTS.batch_search (core/mcts/tree_search/mcts_sampled.py:114-172)
+ * turns each simulation's network outputs into tree inputs with numpy on the host:
+ *   - future agents' actions = argmax of the leaf policy logits       (mcts_sampled.py:116-147)
+ *   - policy probs = softmax of the current agent's logits            (mcts_sampled.py:158-159)
+ *   - beta = probs ** (1 / sampled_tau), renormalised                  (mcts_sampled.py:160-161)
+ * These entry points do the same on the device, in the stream of a tree handle (mzmcts.h), so
+ * the whole simulation loop runs without a host round trip.  Float results are bit-identical to
+ * the numpy expressions on x86-64 numpy 2.x: the exponential restates numpy's float32 SIMD exp
+ * (Cody-Waite reduction, rational minimax P5/Q2 with FMAs, 2^k scaling); sums restate numpy's
+ * pairwise summation (8 interleaved accumulators below 128 elements); float16 inputs follow
+ * numpy's half loops (every operation evaluated in float32 and rounded to half).  The one
+ * exception is sampled_tau != 1 (the reference always passes 1.0, core/config.py:403-404), where
+ * the power uses the device powf.
+ *
+ * Exported only by the product library (mazero_amd/_build/libmzmcts.so); device memory only.
+ */
+#ifndef MZDRIVER_H
+#define MZDRIVER_H
+
+#include <stdint.h>
+
+#include "mzmcts.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mz_dtype { MZ_DT_F32 = 0, MZ_DT_F16 = 1 };
+
+/* Give the handle a new random_seed, as if it had been destroyed and created again with the same
+ * geometry (the reference builds a fresh cytree.Tree_batch per search with seed
+ * np_random.choice(256), mcts_sampled.py:89).  Takes effect at the next mz_prepare; lets a driver
+ * keep one device arena across searches. */
+int mz_reseed(mz_batch *b, uint32_t random_seed);
+
+/* Policy glue of one simulation (mcts_sampled.py:156-161 and 169-170).
+ * logits: the network's policy logits [B, num_agents, A] (row stride `row_stride` elements,
+ * the current agent's A logits start at element `col_offset` of a row), dtype `dtype`.
+ * probs_out, beta_out: float32 [B, A] (= [B, 1, A]). */
+int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
+                   float sampled_tau, float *probs_out, float *beta_out);
+
+/* Estimated joint action of one simulation (mcts_sampled.py:116-147):
+ *   joint[i, k] = factor[i, k]                      for k <  current_agent  (factor int32 [B, factor_cols])
+ *   joint[i, k] = actions[i]                        for k == current_agent  (selection output, int32 [B])
+ *   joint[i, k] = argmax_a pred_logits[i, k, a]     for k >  current_agent  (numpy argmax: first
+ *                                                    maximum, first NaN wins)
+ * pred_logits: [B, num_agents, A] of dtype `dtype`, contiguous (may be NULL when no agent follows
+ * current_agent); joint_out: int64 [B, num_agents]. */
+int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_agents, int current_agent,
+                    const int32_t *factor, int factor_cols, const int32_t *actions, int64_t *joint_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MZDRIVER_H */

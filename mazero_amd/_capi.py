@@ -1,4 +1,4 @@
-"""ctypes binding of the C-ABI declared in include/mzmcts.h.
+"""ctypes binding of the C-ABI declared in include/mzmcts.h and include/mzdriver.h.
 
 `bind(lib)` declares argument/return types on any shared library exporting that ABI.  The product
 loads its own HIP library through `mazero_amd._lib.load()`; the tests use the same binder on the
@@ -89,6 +89,15 @@ _i = C.c_int
 _f = C.c_float
 _i64 = C.c_int64
 
+# include/mzdriver.h (device glue of the driver loop; exported by the product library only)
+MZ_DT_F32, MZ_DT_F16 = 0, 1
+DRIVER_SIGNATURES = {
+    "mz_reseed": (_i, [_p, C.c_uint32]),
+    "mz_policy_glue": (_i, [_p, _p, _i, _i64, _i64, _f, _p, _p]),
+    "mz_joint_action": (_i, [_p, _p, _i, _i, _i, _p, _i, _p, _p]),
+}
+DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
+
 
 def bind(lib: C.CDLL) -> C.CDLL:
     sig = {
@@ -117,6 +126,8 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "mz_get_stats": (_i, [_p, _p]),
         "mz_print": (_i, [_p]),
     }
+    if hasattr(lib, "mz_policy_glue"):  # include/mzdriver.h: product library only
+        sig.update(DRIVER_SIGNATURES)
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res

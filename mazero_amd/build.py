@@ -17,7 +17,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "mzmcts.hip")
+SRCS = [os.path.join(HERE, "csrc", "mzmcts.hip"), os.path.join(HERE, "csrc", "mzdriver.hip")]
+SRC = SRCS[0]
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libmzmcts.so")
 LIB_STAMPS = os.path.join(OUT_DIR, "libmzmcts_stamps.so")  # diagnostic build (MZ_STAMPS=1)
@@ -48,7 +49,8 @@ def needs_build(lib: str = LIB) -> bool:
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = [SRC, os.path.join(ROOT, "include", "mzmcts.h"), __file__]
+    deps = [*SRCS, os.path.join(HERE, "csrc", "mz_internal.h"), os.path.join(ROOT, "include", "mzmcts.h"),
+            os.path.join(ROOT, "include", "mzdriver.h"), __file__]
     return any(os.path.getmtime(p) > t for p in deps)
 
 
@@ -59,7 +61,7 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> st
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = lib + ".tmp"
     extra = ["-DMZ_STAMPS=1"] if stamps else []
-    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), SRC, "-o", tmp]
+    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), *SRCS, "-o", tmp]
     if verbose:
         print("[mazero_amd] " + " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

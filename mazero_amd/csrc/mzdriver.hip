@@ -1,0 +1,215 @@
+// mzdriver.hip — device glue of the sampled-MCTS driver loop (include/mzdriver.h).
+//
+// The reference driver (core/mcts/tree_search/mcts_sampled.py:114-172) moves every simulation's
+// network outputs to the host and prepares the next tree inputs with numpy.  These kernels do the
+// same arithmetic on the device, one wavefront per root, so that the results equal the numpy
+// expressions bit for bit:
+//   - np.exp on float32: numpy 2.x's SIMD float32 exponential (AVX512F and AVX2/FMA3 loops; same
+//     algorithm): k = rint(x * log2 e); y = x + k*(-ln2_hi) + k*(-ln2_lo) with FMAs; exp(y) = P5(y)
+//     / Q2(y), Horner with FMAs; result scaled by 2^k.  Validated here against np.exp on ~2e7
+//     float32 inputs including the denormal range (tests/test_driver.py checks it on every host).
+//   - np.sum(axis=-1) of a contiguous row of n <= 128 elements: pairwise summation base case, 8
+//     interleaved accumulators r[j] += a[i + j], combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
+//     then the n % 8 tail; n < 8 sums sequentially from 0.
+//   - float16 arrays (policy logits under torch autocast): numpy's half loops evaluate each
+//     operation in float32 and round the result to half; half sums accumulate in float32 and
+//     round once.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/mzdriver.h"
+#include "mz_internal.h"
+
+namespace {
+
+constexpr int kWave = 64;
+
+// numpy's float32 exp constants (rational minimax approximation on [-ln2/2, ln2/2]).
+constexpr float kLog2e = 1.442695040888963387f;
+constexpr float kLn2Hi = -6.93145752e-1f;
+constexpr float kLn2Lo = -1.42860677e-6f;
+constexpr float kP0 = 9.999999999980870924916e-01f;
+constexpr float kP1 = 7.257664613233124478488e-01f;
+constexpr float kP2 = 2.473615434895520810817e-01f;
+constexpr float kP3 = 5.114512081637298353406e-02f;
+constexpr float kP4 = 6.757896990527504603057e-03f;
+constexpr float kP5 = 5.082762527590693718096e-04f;
+constexpr float kQ0 = 1.0f;
+constexpr float kQ1 = -2.742335390411667452936e-01f;
+constexpr float kQ2 = 2.159509375685829852307e-02f;
+
+__device__ float np_expf(float x) {
+    if (x != x) return x + x;                 // NaN
+    if (x > 88.72283935546875f) return INFINITY;
+    if (x < -104.0f) return 0.0f;             // below half the smallest denormal
+    const float k = rintf(x * kLog2e);        // product rounded to f32, then to nearest even
+    float y = fmaf(k, kLn2Hi, x);
+    y = fmaf(k, kLn2Lo, y);
+    float num = fmaf(kP5, y, kP4);
+    num = fmaf(num, y, kP3);
+    num = fmaf(num, y, kP2);
+    num = fmaf(num, y, kP1);
+    num = fmaf(num, y, kP0);
+    float den = fmaf(kQ2, y, kQ1);
+    den = fmaf(den, y, kQ0);
+    return ldexpf(num / den, (int)k);
+}
+
+__device__ __forceinline__ float to_half_and_back(float v) { return __half2float(__float2half_rn(v)); }
+
+template <bool F16>
+__device__ __forceinline__ float round_as(float v) {
+    if constexpr (F16) return to_half_and_back(v);
+    return v;
+}
+
+template <bool F16>
+__device__ __forceinline__ float load_elem(const void *p, long long i) {
+    if constexpr (F16) return __half2float(static_cast<const __half *>(p)[i]);
+    return static_cast<const float *>(p)[i];
+}
+
+// numpy pairwise-sum base case over lds[0..n), n <= 128; result broadcast to every lane.
+__device__ float np_row_sum(float v, int l, int n, float *lds, float *acc) {
+    if (l < n) lds[l] = v;
+    __syncthreads();
+    if (n >= 8 && l < 8) {
+        const int n8 = n - n % 8;
+        float r = lds[l];
+        for (int i = 8; i < n8; i += 8) r += lds[i + l];
+        acc[l] = r;
+    }
+    __syncthreads();
+    if (l == 0) {
+        float res;
+        if (n < 8) {
+            res = 0.f;
+            for (int i = 0; i < n; ++i) res += lds[i];
+        } else {
+            res = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+            for (int i = n - n % 8; i < n; ++i) res += lds[i];
+        }
+        acc[8] = res;
+    }
+    __syncthreads();
+    const float out = acc[8];
+    __syncthreads();
+    return out;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+
+// mcts_sampled.py:158-161 (+ .astype(np.float32), :169-170) for root blockIdx.x.
+template <bool F16>
+__global__ __launch_bounds__(kWave) void k_policy_glue(const void *logits, long long row_stride, long long col_off,
+                                                       int A, int use_pow, float tau_inv, float *probs,
+                                                       float *beta) {
+    __shared__ float lds[kWave];
+    __shared__ float acc[9];
+    const int t = blockIdx.x;
+    const int l = threadIdx.x;
+    const bool on = l < A;
+    const float x = on ? load_elem<F16>(logits, (long long)t * row_stride + col_off + l) : -INFINITY;
+    // np.max(..., axis=-1): NaN propagates
+    const bool nan_any = __ballot(on && (x != x)) != 0;
+    const float m = nan_any ? NAN : wave_max(on ? x : -INFINITY);
+    const float d = round_as<F16>(x - m);
+    const float e = round_as<F16>(np_expf(d));
+    const float s = round_as<F16>(np_row_sum(e, l, A, lds, acc));
+    const float p = round_as<F16>(e / s);
+    // `** (1 / sampled_tau)`: numpy returns the array itself for an exponent of 1.0
+    const float q = use_pow ? round_as<F16>(powf(p, tau_inv)) : p;
+    const float s2 = round_as<F16>(np_row_sum(q, l, A, lds, acc));
+    const float b = round_as<F16>(q / s2);
+    if (on) {
+        probs[(long long)t * A + l] = p;
+        beta[(long long)t * A + l] = b;
+    }
+}
+
+// mcts_sampled.py:116-147 for root blockIdx.x: previous agents from `factor`, the current agent
+// from the selection, the following agents by numpy argmax of the leaf policy logits.
+template <bool F16>
+__global__ __launch_bounds__(kWave) void k_joint_action(const void *pred, int N, int A, int cur, const int *factor,
+                                                        int fcols, const int *actions, long long *joint) {
+    const int t = blockIdx.x;
+    const int l = threadIdx.x;
+    if (l < N && l <= cur) joint[(long long)t * N + l] = (l < cur) ? (long long)factor[(long long)t * fcols + l]
+                                                                    : (long long)actions[t];
+    for (int k = cur + 1; k < N; ++k) {
+        const bool on = l < A;
+        const float v = on ? load_elem<F16>(pred, ((long long)t * N + k) * A + l) : -INFINITY;
+        const unsigned long long nan_mask = __ballot(on && (v != v));
+        int idx;
+        if (nan_mask) {
+            idx = __ffsll((long long)nan_mask) - 1;
+        } else {
+            const float m = wave_max(v);
+            idx = __ffsll((long long)__ballot(on && v == m)) - 1;
+        }
+        if (l == 0) joint[(long long)t * N + k] = idx;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
+                   float sampled_tau, float *probs_out, float *beta_out) {
+    int B = 0, A = 0;
+    hipStream_t stream = nullptr;
+    int rc = mz_internal_launch_info(b, &B, &A, &stream);
+    if (rc) return rc;
+    if (!logits || !probs_out || !beta_out) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: null buffer");
+    if (dtype != MZ_DT_F32 && dtype != MZ_DT_F16) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: bad dtype");
+    if (row_stride < A || col_offset < 0 || col_offset + A > row_stride)
+        return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: logits row does not hold the agent's actions");
+    if (!(sampled_tau > 0.f)) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: sampled_tau must be > 0");
+    const float tau_inv = (float)(1.0 / (double)sampled_tau);
+    const int use_pow = (1.0 / (double)sampled_tau) != 1.0;
+    if (dtype == MZ_DT_F16)
+        hipLaunchKernelGGL(k_policy_glue<true>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
+                           (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out);
+    else
+        hipLaunchKernelGGL(k_policy_glue<false>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
+                           (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    return MZ_OK;
+}
+
+int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_agents, int current_agent,
+                    const int32_t *factor, int factor_cols, const int32_t *actions, int64_t *joint_out) {
+    int B = 0, A = 0;
+    hipStream_t stream = nullptr;
+    int rc = mz_internal_launch_info(b, &B, &A, &stream);
+    if (rc) return rc;
+    if (num_agents < 1 || num_agents > kWave || current_agent < 0 || current_agent >= num_agents)
+        return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: bad agent index / count");
+    if (!actions || !joint_out) return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: null buffer");
+    if (current_agent > 0 && (!factor || factor_cols < current_agent))
+        return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: factor must hold the previous agents' actions");
+    if (current_agent + 1 < num_agents && !pred_logits)
+        return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: leaf policy logits required for later agents");
+    if (dtype != MZ_DT_F32 && dtype != MZ_DT_F16) return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: bad dtype");
+    if (dtype == MZ_DT_F16)
+        hipLaunchKernelGGL(k_joint_action<true>, dim3(B), dim3(kWave), 0, stream, pred_logits, num_agents, A,
+                           current_agent, (const int *)factor, factor_cols, (const int *)actions,
+                           (long long *)joint_out);
+    else
+        hipLaunchKernelGGL(k_joint_action<false>, dim3(B), dim3(kWave), 0, stream, pred_logits, num_agents, A,
+                           current_agent, (const int *)factor, factor_cols, (const int *)actions,
+                           (long long *)joint_out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    return MZ_OK;
+}
+
+}  // extern "C"

@@ -39,6 +39,8 @@
 #include <vector>
 
 #include "../../include/mzmcts.h"
+#include "../../include/mzdriver.h"
+#include "mz_internal.h"
 
 namespace {
 
@@ -1691,6 +1693,27 @@ int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const f
     a.row_bytes = row_bytes;
     a.gather_out = (char *)gather_out;
     return launch_step(b, true, true, a);
+}
+
+// include/mzdriver.h
+int mz_reseed(mz_batch *b, uint32_t seed) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    b->geo.seed = seed;
+    b->prepared = false;
+    return MZ_OK;
+}
+
+// Internal hooks for the driver-glue TU (csrc/mz_internal.h).
+int mz_internal_fail(int code, const char *msg) { return fail(code, msg); }
+
+int mz_internal_launch_info(mz_batch *b, int *B, int *A, hipStream_t *stream) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    *B = b->B;
+    *A = b->A;
+    *stream = b->stream;
+    return MZ_OK;
 }
 
 int mz_gather_rows(mz_batch *b, const void *pool, int64_t stride, int64_t row_bytes, const int32_t *idx_x, void *out) {

@@ -207,6 +207,58 @@ class Tree_batch:
         check(self._lib, rc, "expansion_backup_selection_device")
         return out
 
+    def gather_rows(self, pool, idx_x, out):
+        """out[i] = pool[idx_x[i], i] on the device (mcts_sampled.py:130-134); pool [slots, B, ...]."""
+        self._sync_stream()
+        rc = self._lib.mz_gather_rows(
+            self._h, C.c_void_p(pool.data_ptr()), int(pool.stride(0) * pool.element_size()),
+            int(pool[0, 0].numel() * pool.element_size()), C.c_void_p(idx_x.data_ptr()), C.c_void_p(out.data_ptr()),
+        )
+        check(self._lib, rc, "gather_rows")
+        return out
+
+    def reseed(self, random_seed: int):
+        """Same trees as a fresh Tree_batch(..., random_seed, ...) from the next prepare on
+        (include/mzdriver.h, product library only)."""
+        check(self._lib, self._lib.mz_reseed(self._h, int(random_seed) & 0xFFFFFFFF), "reseed")
+
+    # -- device readbacks (no host synchronisation) -------------------------------------------
+    def get_roots_values_device(self, out=None):
+        dev = torch.device("cuda", torch.cuda.current_device())
+        out = torch.empty(self.root_num, dtype=torch.float32, device=dev) if out is None else out
+        self._sync_stream()
+        check(self._lib, self._lib.mz_get_roots_values(self._h, C.c_void_p(out.data_ptr()), MZ_MEM_DEVICE),
+              "get_roots_values_device")
+        return out
+
+    def get_roots_marginal_device(self, visit_out=None, prior_out=None):
+        """(marginal visit counts int32 [B, N, A], marginal priors f32 [B, N, A]) on the device."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        shape = (self.root_num, self.agent_num, self.action_space_size)
+        visit_out = torch.empty(shape, dtype=torch.int32, device=dev) if visit_out is None else visit_out
+        prior_out = torch.empty(shape, dtype=torch.float32, device=dev) if prior_out is None else prior_out
+        self._sync_stream()
+        check(self._lib, self._lib.mz_get_roots_marginal_visit_count(self._h, C.c_void_p(visit_out.data_ptr()),
+                                                                      MZ_MEM_DEVICE), "marginal_visit_count_device")
+        check(self._lib, self._lib.mz_get_roots_marginal_priors(self._h, C.c_void_p(prior_out.data_ptr()),
+                                                                 MZ_MEM_DEVICE), "marginal_priors_device")
+        return visit_out, prior_out
+
+    def get_roots_sampled_padded_device(self, name: str, discount: float = 0.0, degrees_out=None):
+        """Device form of get_roots_sampled_padded: (tensor [B, maxdeg(*N)], degrees int32 [B])."""
+        B, N = self.root_num, self.agent_num
+        W = self.max_children()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        width = W * N if name == "actions" else W
+        out = torch.empty(B, width, dtype=torch.int32 if name in INT_FIELDS else torch.float32, device=dev)
+        self._sync_stream()
+        rc = self._lib.mz_get_roots_sampled_padded(
+            self._h, FIELDS[name], float(discount), C.c_void_p(out.data_ptr()),
+            C.c_void_p(degrees_out.data_ptr()) if degrees_out is not None else None, MZ_MEM_DEVICE,
+        )
+        check(self._lib, rc, f"get_roots_sampled_{name}_device")
+        return out, degrees_out
+
     # -- readbacks (cytree.pyx:93-241) ----------------------------------------------------------
     def get_roots_values(self):
         out = np.empty(self.root_num, np.float32)

@@ -1,0 +1,278 @@
+"""Device-resident `SampledMCTS.batch_search` — drop-in for the reference driver
+core/mcts/tree_search/mcts_sampled.py:29-200.
+
+Same constructor, same `batch_search` signature, same `SearchOutput` (numpy arrays and per-root
+lists).  What changes is where the loop runs.  The reference moves every simulation's network
+outputs to the host, prepares the next tree inputs with numpy and calls the CPU tree three times
+per simulation.  Here the tree (mazero_amd.cytree on the MI355X library), the hidden-state pool
+and the per-simulation glue stay on the device:
+
+    select(s+1) + gather leaf rows          one kernel (fused with expand/backup of s)
+    model.prediction(leaf)                  the model's own kernels (only when later agents exist)
+    joint action                            mz_joint_action (numpy argmax semantics)
+    model.dynamics + model.prediction       the model's own kernels, inverse transforms included
+    policy softmax + beta                   mz_policy_glue (numpy float32/float16 arithmetic)
+
+so a search has no host synchronisation between `prepare` and the final readback.  Root
+preprocessing stays on the host in numpy, exactly as the reference does it
+(mcts_sampled.py:51-106): it consumes `np_random` (Dirichlet noise, then the tree seed) and runs
+once per search.
+
+Model interface (core/model.py:45-79): `prediction(h) -> (policy_logits [B,N,A], value_logits)`,
+`dynamics(h, joint_action [B,N]) -> (next_h, reward_logits)`, `inverse_value_transform`,
+`inverse_reward_transform`; this is what MAMuZeroNet.recurrent_inference does in eval mode
+(config/smac/model.py:562-572) minus the host copies.  A model may instead provide
+`recurrent_inference_device(h, action) -> (next_h, reward [B,1], value [B,1], policy_logits)`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, NamedTuple, Tuple
+
+import numpy as np
+import torch
+
+from ._capi import MZ_DT_F16, MZ_DT_F32, check
+from .cytree import Tree_batch
+
+
+class SearchOutput(NamedTuple):
+    """mcts_sampled.py:12-26."""
+
+    value: np.ndarray
+    marginal_visit_count: np.ndarray
+    marginal_priors: np.ndarray
+    sampled_actions: List[np.ndarray]
+    sampled_visit_count: List[np.ndarray]
+    sampled_pred_probs: List[np.ndarray]
+    sampled_beta: List[np.ndarray]
+    sampled_beta_hat: List[np.ndarray]
+    sampled_priors: List[np.ndarray]
+    sampled_imp_ratio: List[np.ndarray]
+    sampled_pred_values: List[np.ndarray]
+    sampled_mcts_values: List[np.ndarray]
+    sampled_rewards: List[np.ndarray]
+    sampled_qvalues: List[np.ndarray]
+
+
+_SAMPLED_FIELDS = ("actions", "visit_count", "pred_probs", "beta", "beta_hat", "priors", "imp_ratio",
+                   "pred_values", "mcts_values", "rewards", "qvalues")
+
+
+class DeviceSearchOutput(NamedTuple):
+    """The search results as device tensors: per-root lists padded to the widest root degree
+    (`degrees[i]` valid entries in row i).  `to_host()` gives the reference's SearchOutput."""
+
+    value: torch.Tensor                  # f32 [B]
+    marginal_visit_count: torch.Tensor   # i32 [B, 1, A]
+    marginal_priors: torch.Tensor        # f32 [B, 1, A]
+    degrees: torch.Tensor                # i32 [B]
+    sampled: dict                        # field -> [B, maxdeg] (i32 for actions / visit_count)
+
+    def to_host(self) -> SearchOutput:
+        deg = self.degrees.cpu().numpy()
+        host = {k: v.cpu().numpy() for k, v in self.sampled.items()}
+        B = deg.shape[0]
+
+        def lists(name):
+            a = host[name]
+            if name == "actions":
+                return [np.ascontiguousarray(a[i, : deg[i]]).reshape(deg[i], 1) for i in range(B)]
+            return [np.ascontiguousarray(a[i, : deg[i]]) for i in range(B)]
+
+        return SearchOutput(self.value.cpu().numpy(), self.marginal_visit_count.cpu().numpy(),
+                            self.marginal_priors.cpu().numpy(), *[lists(f) for f in _SAMPLED_FIELDS])
+
+
+def _np(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return MZ_DT_F32
+    if t.dtype == torch.float16:
+        return MZ_DT_F16
+    raise TypeError(f"policy logits must be float32 or float16, got {t.dtype}")
+
+
+# One device arena per search geometry, kept across searches and across SampledMCTS instances (the
+# self-play worker makes a new SampledMCTS every environment step, selfplay_worker.py:187); a
+# search reseeds it instead of allocating a new tree batch as the reference does (:89).
+_TREES: dict = {}
+
+
+class SampledMCTS:
+    """mcts_sampled.py:29-32.  `lib` selects the tree library (default: the MI355X product)."""
+
+    def __init__(self, config, np_random: np.random.RandomState = None, *, lib=None):
+        self.config = config
+        self.np_random = np.random if np_random is None else np_random
+        self._lib = lib
+
+    # ---------------------------------------------------------------------------------------
+    def root_inputs(self, network_output, current_agent_idx, legal_actions_lst, add_noise, sampled_tau):
+        """Root preprocessing, mcts_sampled.py:51-106, in numpy on the host (it draws from
+        np_random).  Returns the prepare() arguments and the tree seed."""
+        cfg = self.config
+        alpha, eps = cfg.root_dirichlet_alpha, cfg.root_exploration_fraction
+        A = cfg.action_space_size
+        B = network_output.hidden_state.shape[0]
+        logits = _np(network_output.policy_logits)[:, current_agent_idx, :].reshape(B, 1, A)
+        # softmax in the logits' own dtype (float16 under autocast), :64-65
+        probs = np.exp(logits - np.max(logits, axis=-1, keepdims=True))
+        probs = probs / np.sum(probs, axis=-1, keepdims=True)
+        # Dirichlet noise is always drawn, then disabled for evaluation, :68-70
+        noises = self.np_random.dirichlet([alpha] * A, B).astype(np.float32).reshape(B, 1, A)
+        if not add_noise:
+            eps = 0.0
+        mask = None
+        if legal_actions_lst is not None:  # :73-83
+            mask = legal_actions_lst[:, current_agent_idx, :].reshape(B, 1, A)
+            probs *= mask
+            probs += mask * 1e-4
+            probs = probs / np.sum(probs, axis=-1, keepdims=True)
+            noises *= mask
+            noises += mask * 1e-4
+            noises = noises / np.sum(noises, axis=-1, keepdims=True)
+        seed = self.np_random.choice(256)  # drawn after the noise, :89
+        beta = probs * (1 - eps) + noises * eps  # :93-100
+        beta = beta ** (1 / sampled_tau)
+        if mask is not None:
+            beta *= mask
+        beta = beta / np.sum(beta, axis=-1, keepdims=True)
+        rewards = _np(network_output.reward).reshape(B).astype(np.float32)
+        values = _np(network_output.value).reshape(B).astype(np.float32)
+        return (rewards, values, probs.astype(np.float32), beta.astype(np.float32), eps,
+                noises.astype(np.float32, copy=False)), seed
+
+    def _tree(self, B, seed, device):
+        cfg = self.config
+        key = (B, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
+               float(cfg.tree_value_stat_delta_lb), float(cfg.mcts_rho), float(cfg.mcts_lambda), str(device),
+               id(self._lib))
+        tb = _TREES.get(key)
+        if tb is None:
+            tb = Tree_batch(B, 1, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
+                            cfg.tree_value_stat_delta_lb, int(seed), cfg.mcts_rho, cfg.mcts_lambda, lib=self._lib)
+            _TREES[key] = tb
+        else:
+            tb.reseed(int(seed))
+        return tb
+
+    # ---------------------------------------------------------------------------------------
+    def batch_search(self, model, network_output, current_agent_idx: int, factor: np.ndarray,
+                     true_num_agents: int, legal_actions_lst: np.ndarray = None, device: torch.device = None,
+                     add_noise: bool = False, sampled_tau: float = 1.0,
+                     sampled_actions_res: Tuple[np.ndarray, np.ndarray] = None) -> SearchOutput:
+        """mcts_sampled.py:34-200; results identical to the reference driver given the same model."""
+        out = self.batch_search_device(model, network_output, current_agent_idx, factor, true_num_agents,
+                                       legal_actions_lst, device, add_noise, sampled_tau, sampled_actions_res,
+                                       _host_readback=True)
+        return out
+
+    def batch_search_device(self, model, network_output, current_agent_idx: int, factor, true_num_agents: int,
+                            legal_actions_lst=None, device=None, add_noise: bool = False, sampled_tau: float = 1.0,
+                            sampled_actions_res=None, _host_readback: bool = False):
+        """The search with device-resident outputs (DeviceSearchOutput), for on-device consumers."""
+        if sampled_actions_res is not None:
+            raise NotImplementedError  # as the reference, mcts_sampled.py:108-109
+        cfg = self.config
+        c2, c1, disc = cfg.pb_c_base, cfg.pb_c_init, cfg.discount
+        A, K, S = cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations
+        N, cur = int(true_num_agents), int(current_agent_idx)
+        hidden = network_output.hidden_state
+        if not (isinstance(hidden, torch.Tensor) and hidden.is_cuda):
+            raise ValueError("network_output.hidden_state must be a GPU tensor")
+        dev = hidden.device
+        B = hidden.shape[0]
+
+        (rr, rv, rp, rb, eps, rn), seed = self.root_inputs(network_output, cur, legal_actions_lst, add_noise,
+                                                           sampled_tau)
+        with torch.cuda.device(dev):
+            tb = self._tree(B, seed, dev)
+            lib, h = tb._lib, tb._h
+            up = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (rr, rv, rp, rb, rn)]
+            tb.prepare(up[0], up[1], up[2], up[3], K, eps, up[4])
+
+            row = hidden.reshape(B, -1)
+            idx = torch.empty(B, dtype=torch.int32, device=dev)
+            idy = torch.empty(B, dtype=torch.int32, device=dev)
+            act = torch.empty(B, 1, dtype=torch.int32, device=dev)
+            sel = (idx, idy, act)
+            joint = torch.empty(B, N, dtype=torch.int64, device=dev)
+            probs = torch.empty(B, A, dtype=torch.float32, device=dev)
+            beta = torch.empty(B, A, dtype=torch.float32, device=dev)
+            fac = None
+            if cur > 0:
+                fac = torch.from_numpy(np.ascontiguousarray(np.asarray(factor)[:, :cur], dtype=np.int32)).to(dev)
+            pool = None
+            leaf = None
+
+            with torch.no_grad():
+                model.eval()
+                tb.batch_selection_device(c2, c1, disc, out=sel)
+                leaf = row  # simulation 0 selects a child of every root: its parent is the root (slot 0)
+                for s in range(S):
+                    with torch.autocast("cuda"):
+                        if cur + 1 < N:  # later agents' actions from the leaf policy, :136-145
+                            pred_logits, _ = model.prediction(leaf)
+                            pred_logits = pred_logits.contiguous()
+                            ptr, dt = C.c_void_p(pred_logits.data_ptr()), _dtype_code(pred_logits)
+                        else:
+                            ptr, dt = None, MZ_DT_F32
+                        check(lib, lib.mz_joint_action(h, ptr, dt, N, cur,
+                                                       C.c_void_p(fac.data_ptr()) if fac is not None else None,
+                                                       cur, C.c_void_p(act.data_ptr()), C.c_void_p(joint.data_ptr())),
+                              "joint_action")
+                        next_h, reward, value, logits = self._recurrent(model, leaf, joint)  # :150-156
+                    nh = next_h.reshape(B, -1)
+                    if pool is None:
+                        pdt = torch.promote_types(row.dtype, nh.dtype)
+                        pool = torch.empty((S + 1, B, nh.shape[1]), dtype=pdt, device=dev)
+                        pool[0].copy_(row)
+                        leaf = torch.empty((B, nh.shape[1]), dtype=pdt, device=dev)
+                    pool[s + 1].copy_(nh)  # :164
+                    logits = logits.contiguous()
+                    check(lib, lib.mz_policy_glue(h, C.c_void_p(logits.data_ptr()), _dtype_code(logits),
+                                                  logits.shape[1] * logits.shape[2], cur * A, float(sampled_tau),
+                                                  C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr())),
+                          "policy_glue")
+                    r32 = reward.reshape(B).float()
+                    v32 = value.reshape(B).float()
+                    if s + 1 < S:
+                        tb.expansion_backup_selection_device(s + 1, disc, K, r32, v32, probs, beta, c2, c1,
+                                                             out=sel, pool=pool, gather_out=leaf)
+                    else:
+                        tb.batch_expansion_and_backup(s + 1, disc, K, r32, v32, probs, beta)
+
+            if _host_readback:  # :176-191 (one packed device->host copy)
+                return SearchOutput(
+                    tb.get_roots_values(), tb.get_roots_marginal_visit_count(), tb.get_roots_marginal_priors(),
+                    tb.get_roots_sampled_actions(), tb.get_roots_sampled_visit_count(),
+                    tb.get_roots_sampled_pred_probs(), tb.get_roots_sampled_beta(), tb.get_roots_sampled_beta_hat(),
+                    tb.get_roots_sampled_priors(), tb.get_roots_sampled_imp_ratio(),
+                    tb.get_roots_sampled_pred_values(), tb.get_roots_sampled_mcts_values(),
+                    tb.get_roots_sampled_rewards(), tb.get_roots_sampled_qvalues(disc))
+            value = tb.get_roots_values_device()
+            mv, mp = tb.get_roots_marginal_device()
+            deg = torch.empty(B, dtype=torch.int32, device=dev)
+            sampled = {}
+            for f in _SAMPLED_FIELDS:
+                sampled[f], _ = tb.get_roots_sampled_padded_device(f, disc, degrees_out=deg if f == "actions" else None)
+            return DeviceSearchOutput(value, mv, mp, deg, sampled)
+
+    @staticmethod
+    def _recurrent(model, hidden, action):
+        """(next_h, reward [B,1], value [B,1], policy_logits [B,N,A]) on the device, as
+        MAMuZeroNet.recurrent_inference computes them in eval mode (config/smac/model.py:562-572)."""
+        fn = getattr(model, "recurrent_inference_device", None)
+        if fn is not None:
+            return fn(hidden, action)
+        next_h, reward_logits = model.dynamics(hidden, action)
+        policy_logits, value_logits = model.prediction(next_h)
+        reward = model.inverse_reward_transform(reward_logits)
+        value = model.inverse_value_transform(value_logits)
+        return next_h, reward, value, policy_logits

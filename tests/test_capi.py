@@ -1,7 +1,7 @@
 """The C-ABI boundary (CPU only: no device compute here).
 
 * every entry point declared in include/mzmcts.h is exported by the product library and by both
-  oracle libraries
+  oracle libraries; include/mzdriver.h (driver glue) by the product library
 * the product library loads on a machine without a GPU and fails loudly (no silent fallback)
 * the Tree_batch shim mirrors cytree.pyx's argument handling (dtype check -> ValueError,
   invariant violations -> RuntimeError)
@@ -21,11 +21,23 @@ from mazero_amd import _capi
 from mazero_amd.cytree import Tree_batch
 
 HEADER = os.path.join(ROOT, "include", "mzmcts.h")
+DRIVER_HEADER = os.path.join(ROOT, "include", "mzdriver.h")
 
 
-def declared_symbols():
-    txt = open(HEADER).read()
+def declared_symbols(header=HEADER):
+    txt = open(header).read()
     return sorted(set(re.findall(r"\b(mz_[a-z_]+)\s*\(", txt)))
+
+
+def test_driver_header_matches_binding_table():
+    assert declared_symbols(DRIVER_HEADER) == _capi.DRIVER_EXPORTS
+    from mazero_amd import build
+
+    raw = C.CDLL(build.build(verbose=False))
+    for name in _capi.DRIVER_EXPORTS:
+        assert hasattr(raw, name), name
+    # internal hooks of the driver TU stay hidden
+    assert not hasattr(raw, "mz_internal_fail")
 
 
 def test_header_matches_binding_table():

@@ -1,0 +1,296 @@
+"""Device-resident search driver (mazero_amd.mcts_sampled) and its glue kernels
+(include/mzdriver.h), checked against numpy and against the oracle driver (oracle/driver.py, a
+restatement of core/mcts/tree_search/mcts_sampled.py:34-200 over the oracle tree).
+
+CPU tests pin the arithmetic the glue kernels restate:
+- numpy's float32 SIMD exp: the constants are parsed from mzdriver.hip and emulated with exact
+  FMAs;
+- numpy's pairwise summation order.
+GPU tests compare the kernels with numpy bit for bit, then compare whole searches with the
+oracle driver running the same network on the same GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIP = os.path.join(ROOT, "mazero_amd", "csrc", "mzdriver.hip")
+
+
+# ------------------------------------------------------------------------------------------------
+# numpy arithmetic the kernels restate (CPU)
+# ------------------------------------------------------------------------------------------------
+def _kernel_constants():
+    src = open(HIP).read()
+    names = ["kLog2e", "kLn2Hi", "kLn2Lo", "kP0", "kP1", "kP2", "kP3", "kP4", "kP5", "kQ0", "kQ1", "kQ2"]
+    out = {}
+    for n in names:
+        m = re.search(rf"constexpr float {n} = ([-+0-9.eE]+)f;", src)
+        assert m, n
+        out[n] = np.float32(float(m.group(1)))
+    return out
+
+
+def _fma(a, b, c):
+    # float32 operands: the product is exact in float64; one rounding of the sum to float64 and
+    # then to float32 equals the single fused rounding except for double-rounding ties, which
+    # the sweep below would expose as mismatches.
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(np.float32)
+
+
+def np_expf_emulated(x):
+    k = _kernel_constants()
+    x = np.asarray(x, np.float32)
+    q = np.rint((x * k["kLog2e"]).astype(np.float32))
+    full = lambda v: np.full_like(x, v)  # noqa: E731
+    y = _fma(q, full(k["kLn2Hi"]), x)
+    y = _fma(q, full(k["kLn2Lo"]), y)
+    num = _fma(full(k["kP5"]), y, full(k["kP4"]))
+    for c in ("kP3", "kP2", "kP1", "kP0"):
+        num = _fma(num, y, full(k[c]))
+    den = _fma(full(k["kQ2"]), y, full(k["kQ1"]))
+    den = _fma(den, y, full(k["kQ0"]))
+    r = (num / den).astype(np.float32)
+    with np.errstate(all="ignore"):
+        out = np.ldexp(r, np.clip(q, -300, 300).astype(np.int32)).astype(np.float32)
+    out = np.where(x < -104.0, np.float32(0), out)
+    return out
+
+
+def np_row_sum_emulated(a):
+    """numpy's pairwise summation of one contiguous row of n <= 128 float32 values."""
+    a = np.asarray(a, np.float32)
+    n = len(a)
+    if n < 8:
+        r = np.float32(0)
+        for v in a:
+            r = np.float32(r + v)
+        return r
+    acc = list(a[:8])
+    n8 = n - n % 8
+    for i in range(8, n8, 8):
+        for j in range(8):
+            acc[j] = np.float32(acc[j] + a[i + j])
+    res = np.float32(np.float32(np.float32(acc[0] + acc[1]) + np.float32(acc[2] + acc[3]))
+                     + np.float32(np.float32(acc[4] + acc[5]) + np.float32(acc[6] + acc[7])))
+    for i in range(n8, n):
+        res = np.float32(res + a[i])
+    return res
+
+
+def test_numpy_float32_exp_restatement():
+    rng = np.random.default_rng(0)
+    xs = [
+        ((rng.random(1_000_000) * 2 - 1) * 20).astype(np.float32),
+        (-rng.random(500_000) * 110).astype(np.float32),  # softmax range incl. denormals / zero
+        (-110 + 25 * rng.random(500_000)).astype(np.float32),
+        np.arange(0x80000000, 0xBF800001, 4099, dtype=np.uint64).astype(np.uint32).view(np.float32),  # [-1, 0]
+    ]
+    for x in xs:
+        got = np_expf_emulated(x)
+        ref = np.exp(x)
+        bad = np.flatnonzero(got.view(np.uint32) != ref.view(np.uint32))
+        assert bad.size == 0, f"{bad.size} mismatches, e.g. x={x[bad[:3]]} got={got[bad[:3]]} numpy={ref[bad[:3]]}"
+
+
+def test_numpy_pairwise_sum_restatement():
+    rng = np.random.default_rng(1)
+    for n in list(range(1, 70)):
+        X = (rng.random((200, n)) * rng.choice([1e-3, 1.0, 1e3], size=(200, n))).astype(np.float32)
+        S = np.sum(X, axis=-1, keepdims=True)[:, 0]
+        for i in range(200):
+            assert np_row_sum_emulated(X[i]) == S[i], (n, i)
+
+
+def test_numpy_float16_sum_restatement():
+    rng = np.random.default_rng(2)
+    for n in (3, 9, 11, 15, 36):
+        X = rng.random((300, n)).astype(np.float16)
+        S = np.sum(X, axis=-1, keepdims=True)[:, 0]
+        for i in range(300):
+            assert np.float16(np_row_sum_emulated(X[i].astype(np.float32))) == S[i]
+
+
+def _numpy_policy_glue(logits, tau=1.0):
+    """mcts_sampled.py:158-161 + astype(np.float32) (:169-170), in the logits' dtype."""
+    p = np.exp(logits - np.max(logits, axis=-1, keepdims=True))
+    p = p / np.sum(p, axis=-1, keepdims=True)
+    b = p ** (1 / tau)
+    b = b / np.sum(b, axis=-1, keepdims=True)
+    return p.astype(np.float32), b.astype(np.float32)
+
+
+def test_oracle_driver_runs_on_cpu(port_lib):
+    """The oracle driver itself (CPU network, CPU port tree): search invariants."""
+    import torch
+
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+    from driver import OracleSampledMCTS
+
+    N, A, B, S = 3, 9, 6, 12
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=5)
+    net = make_net(N, A, seed=0)
+    out, legal = make_root_batch(net, B, 64, seed=1, device=torch.device("cpu"), legal_zero_frac=0.3)
+    res = OracleSampledMCTS(cfg, np.random.RandomState(0), port_lib).batch_search(
+        net, out, 1, np.zeros((B, 1), np.int32), N, legal, add_noise=True)
+    assert res["marginal_visit_count"].shape == (B, 1, A)
+    assert (res["marginal_visit_count"].sum(axis=(1, 2)) == S).all()
+    for i in range(B):
+        assert res["sampled_visit_count"][i].sum() == S
+        assert legal[i, 1, res["sampled_actions"][i][:, 0]].all()
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU
+# ------------------------------------------------------------------------------------------------
+def _handle(B, A):
+    from mazero_amd.cytree import Tree_batch
+
+    return Tree_batch(B, 1, A, 1, 4, 0.01, 0, 0.75, 0.8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+@pytest.mark.parametrize("A", [3, 9, 15, 36, 64])
+def test_policy_glue_matches_numpy(dtype, A):
+    import torch
+
+    from mazero_amd._capi import MZ_DT_F16, MZ_DT_F32, check
+
+    B, N, cur = 512, 3, 1
+    rng = np.random.default_rng(A)
+    logits = (rng.standard_normal((B, N, A)) * rng.choice([0.1, 1, 4, 30], size=(B, 1, 1))).astype(dtype)
+    logits[:7, cur, 0] = -np.inf          # masked-out actions
+    logits[7:14, cur, :] = logits[7:14, cur, :1]  # all-equal rows
+    if A > 1:
+        logits[14:20, cur, 1] = 60.0      # one dominant logit (others underflow)
+    tb = _handle(B, A)
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(logits).to(dev)
+    probs = torch.empty(B, A, device=dev)
+    beta = torch.empty(B, A, device=dev)
+    tb._sync_stream()
+    rc = tb._lib.mz_policy_glue(tb._h, C.c_void_p(x.data_ptr()), MZ_DT_F16 if dtype == "float16" else MZ_DT_F32,
+                                N * A, cur * A, 1.0, C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr()))
+    check(tb._lib, rc, "policy_glue")
+    with np.errstate(all="ignore"):
+        ep, eb = _numpy_policy_glue(logits[:, cur, :].reshape(B, 1, A))
+    gp, gb = probs.cpu().numpy(), beta.cpu().numpy()
+    np.testing.assert_array_equal(gp.view(np.uint32), ep.reshape(B, A).view(np.uint32))
+    np.testing.assert_array_equal(gb.view(np.uint32), eb.reshape(B, A).view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+def test_joint_action_matches_numpy(dtype):
+    import torch
+
+    from mazero_amd._capi import MZ_DT_F16, MZ_DT_F32, check
+
+    B, N, A = 300, 5, 11
+    rng = np.random.default_rng(7)
+    pred = rng.integers(-3, 3, size=(B, N, A)).astype(dtype)  # many ties
+    pred[:10, 3, 4] = np.nan
+    pred[10:20, 4, :] = pred[10:20, 4, :1]
+    dev = torch.device("cuda", 0)
+    tb = _handle(B, A)
+    for cur in range(N):
+        factor = rng.integers(0, A, size=(B, max(cur, 1))).astype(np.int32)
+        act = rng.integers(0, A, size=B).astype(np.int32)
+        joint = torch.empty(B, N, dtype=torch.int64, device=dev)
+        p, f, a = (torch.from_numpy(v).to(dev) for v in (pred, factor, act))
+        tb._sync_stream()
+        rc = tb._lib.mz_joint_action(tb._h, C.c_void_p(p.data_ptr()), MZ_DT_F16 if dtype == "float16" else MZ_DT_F32,
+                                     N, cur, C.c_void_p(f.data_ptr()), factor.shape[1], C.c_void_p(a.data_ptr()),
+                                     C.c_void_p(joint.data_ptr()))
+        check(tb._lib, rc, "joint_action")
+        exp = np.zeros((B, N), np.int64)  # mcts_sampled.py:116-145
+        exp[:, :cur] = factor[:, :cur]
+        exp[:, cur] = act
+        for k in range(cur + 1, N):
+            exp[:, k] = np.argmax(pred[:, k, :], axis=-1)
+        np.testing.assert_array_equal(joint.cpu().numpy(), exp)
+
+
+def _compare_outputs(got, exp):
+    for name in exp:
+        g = getattr(got, name)
+        e = exp[name]
+        if isinstance(e, list):
+            assert len(g) == len(e), name
+            for i, (gi, ei) in enumerate(zip(g, e)):
+                assert gi.dtype == ei.dtype and gi.shape == ei.shape, (name, i, gi.dtype, ei.dtype, gi.shape, ei.shape)
+                np.testing.assert_array_equal(gi.view(np.uint32) if gi.dtype == np.float32 else gi,
+                                              ei.view(np.uint32) if ei.dtype == np.float32 else ei, err_msg=f"{name}[{i}]")
+        else:
+            assert g.dtype == e.dtype and g.shape == e.shape, name
+            np.testing.assert_array_equal(g.view(np.uint32) if g.dtype == np.float32 else g,
+                                          e.view(np.uint32) if e.dtype == np.float32 else e, err_msg=name)
+
+
+DRIVER_CASES = [
+    # (N, A, B, S, K, agent, legal_zero_frac, add_noise, float_policy)
+    (3, 9, 64, 20, 1, 0, 0.0, True, False),
+    (3, 9, 64, 20, 5, 1, 0.3, True, False),
+    (3, 9, 64, 20, 5, 2, 0.3, False, False),
+    (5, 11, 48, 16, 10, 2, 0.2, True, True),
+    (2, 3, 8, 25, 5, 0, 0.0, True, True),
+    (8, 15, 32, 30, 5, 5, 0.3, True, False),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", DRIVER_CASES, ids=lambda c: f"N{c[0]}A{c[1]}B{c[2]}S{c[3]}K{c[4]}ag{c[5]}")
+def test_driver_matches_oracle_driver(case, port_lib):
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, B, S, K, cur, zf, noise, fpol = case
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=K)
+    net = make_net(N, A, seed=3, device=dev, float_policy=fpol)
+    out, legal = make_root_batch(net, B, 64, seed=4, device=dev, legal_zero_frac=zf)
+    factor = np.random.default_rng(5).integers(0, A, size=(B, max(cur, 1))).astype(np.int32)[:, :cur] if cur else None
+    exp = OracleSampledMCTS(cfg, np.random.RandomState(11), port_lib).batch_search(
+        net, out, cur, factor, N, legal, device=dev, add_noise=noise)
+    got = SampledMCTS(cfg, np.random.RandomState(11)).batch_search(
+        net, out, cur, factor, N, legal, device=dev, add_noise=noise)
+    _compare_outputs(got, exp)
+
+
+@pytest.mark.gpu
+def test_driver_device_outputs_and_reuse(port_lib):
+    """Back-to-back searches reuse one device arena (reseeded); the device-output form agrees
+    with the host form; the np_random stream advances exactly as the reference's."""
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, B, S = 3, 9, 32, 15
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=3)
+    net = make_net(N, A, seed=8, device=dev)
+    out, legal = make_root_batch(net, B, 64, seed=9, device=dev, legal_zero_frac=0.2)
+    rs_o, rs_d = np.random.RandomState(21), np.random.RandomState(21)
+    oracle = OracleSampledMCTS(cfg, rs_o, port_lib)
+    drv = SampledMCTS(cfg, rs_d)
+    for agent in range(N):  # the self-play agent loop, selfplay_worker.py:196-211
+        factor = np.zeros((B, agent), np.int32) if agent else None
+        exp = oracle.batch_search(net, out, agent, factor, N, legal, device=dev, add_noise=True)
+        if agent == 1:
+            dout = drv.batch_search_device(net, out, agent, factor, N, legal, device=dev, add_noise=True)
+            got = dout.to_host()
+        else:
+            got = drv.batch_search(net, out, agent, factor, N, legal, device=dev, add_noise=True)
+        _compare_outputs(got, exp)
+    assert rs_o.randint(1 << 30) == rs_d.randint(1 << 30)
