@@ -1,0 +1,118 @@
+"""Secondary benchmark: the whole search loop with a network (SURVEY.md §8d "Full-loop").
+
+One step = one environment step of the self-play loop (selfplay_worker.py:187-211): the N agents
+of the map are searched one after another with `SampledMCTS.batch_search`, each over B roots x S
+simulations, with the network on the GPU. The network is `mazero_amd.nets.MuZeroShapedNet`:
+the SMAC MAMuZeroNet's shapes with MLP heads and random weights, run under autocast as the
+reference runs it.
+
+Reported, as one JSON line:
+- `device`: mazero_amd.mcts_sampled.SampledMCTS. The tree, pool and glue are on the GPU, and
+  the search loop is captured in a HIP graph after the first search of each configuration.
+- `device_eager`: the same driver without graphs.
+- `reference_loop` (when oracle/_ref is built): the reference driver restated in
+  oracle/driver.py, i.e. numpy glue, vstack gathers and the reference C++ ctree on one host
+  core, driving the same GPU network. This is what a reference self-play step costs on this
+  machine. Its results are checked bit for bit against `device` on the first step.
+
+This is not the headline metric (bench.py is); the network is synthetic and its cost is the
+same for both.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+MAPS = {"3m": (3, 9), "2s3z": (5, 11), "3s5z_vs_3s6z": (8, 15), "27m_vs_30m": (27, 36)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--map", default="3m", choices=sorted(MAPS))
+    ap.add_argument("--roots", type=int, default=256)
+    ap.add_argument("--sims", type=int, default=50)
+    ap.add_argument("--sampled-times", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--ref-steps", type=int, default=2)
+    ap.add_argument("--no-ref", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A = MAPS[args.map]
+    B, S, K = args.roots, args.sims, args.sampled_times
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=K)
+    net = make_net(N, A, seed=0, device=dev)
+    roots = [make_root_batch(net, B, 64, seed=10 + i, device=dev, legal_zero_frac=0.2) for i in range(3)]
+
+    def env_step(mcts, i):
+        out, legal = roots[i % len(roots)]
+        acts = np.zeros((B, N), np.int32)
+        res = None
+        for agent in range(N):  # selfplay_worker.py:196-211
+            factor = acts[:, :agent].copy() if agent else None
+            res = mcts.batch_search(net, out, agent, factor, N, legal, device=dev, add_noise=True)
+            acts[:, agent] = [int(a[np.argmax(v), 0]) if len(a) else 0
+                              for a, v in zip(res.sampled_actions, res.sampled_visit_count)]
+        return res
+
+    def timed(mcts, steps, warm):
+        for i in range(warm):
+            env_step(mcts, i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            env_step(mcts, i)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    sims_per_step = B * S * N
+    line = {"metric": f"full search loop simulations/s, SMAC {args.map} ({N} agents x {B} roots x {S} sims, K={K})",
+            "unit": "simulations/s", "network": "MuZeroShapedNet (MLP heads, random init, autocast)"}
+    t = timed(SampledMCTS(cfg, np.random.RandomState(0), use_graph=True), args.steps, 2)
+    line["device"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3)}
+    t = timed(SampledMCTS(cfg, np.random.RandomState(0), use_graph=False), max(1, args.steps // 2), 1)
+    line["device_eager"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3)}
+
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libmzref.so")
+    if not args.no_ref and os.path.exists(ref_path):
+        import ctypes as C
+
+        from driver import OracleSampledMCTS
+        from mazero_amd import _capi
+
+        lib = _capi.bind(C.CDLL(ref_path))
+
+        class _Adapter(OracleSampledMCTS):
+            def batch_search(self, *a, **k):
+                from mazero_amd.mcts_sampled import SearchOutput
+
+                return SearchOutput(**super().batch_search(*a, **k))
+
+        # parity spot check on one env step
+        a = env_step(_Adapter(cfg, np.random.RandomState(7), lib), 0)
+        b = env_step(SampledMCTS(cfg, np.random.RandomState(7)), 0)
+        same = all(np.array_equal(np.asarray(x), np.asarray(y)) if not isinstance(x, list)
+                   else all(np.array_equal(u, v) for u, v in zip(x, y)) for x, y in zip(a, b))
+        t = timed(_Adapter(cfg, np.random.RandomState(0), lib), args.ref_steps, 0)
+        line["reference_loop"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3),
+                                  "tree": "reference ctree (oracle/_ref), 1 host core", "bit_exact_vs_device": same}
+        line["speedup_vs_reference_loop"] = round(line["device"]["value"] / line["reference_loop"]["value"], 2)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

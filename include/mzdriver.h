@@ -36,6 +36,12 @@ enum mz_dtype { MZ_DT_F32 = 0, MZ_DT_F16 = 1 };
  * keep one device arena across searches. */
 int mz_reseed(mz_batch *b, uint32_t random_seed);
 
+/* Tell the handle that its trees were changed by work it did not enqueue itself -- the replay of
+ * a captured graph of mz_* calls -- so that host-side readback caches are dropped.  (Captured
+ * launches read the seed and every input from device memory, so a replay after mz_reseed and
+ * fresh input copies is a new search.) */
+int mz_state_changed(mz_batch *b);
+
 /* Policy glue of one simulation (mcts_sampled.py:156-161 and 169-170).
  * logits: the network's policy logits [B, num_agents, A] (row stride `row_stride` elements,
  * the current agent's A logits start at element `col_offset` of a row), dtype `dtype`.

@@ -100,6 +100,7 @@ struct Dev {
     float *pb;   // [PS] logf((n + c2 + 1)/c2) + c1
     double *sq;  // [PS] sqrt(n)
     float *lp;   // [PS+1] lambda^d as a float chain
+    unsigned *seed;  // [1] random_seed, read by k_prepare (device-side so captured graphs follow mz_reseed)
 };
 
 struct StepArgs {
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
     const int t = blockIdx.x;
     const int tid = threadIdx.x;
     if (tid == 0) {  // std::mt19937::seed: sequential by definition
-        unsigned x = g.seed * 2333u + (unsigned)(g.root_offset + t);
+        unsigned x = d.seed[0] * 2333u + (unsigned)(g.root_offset + t);
         mt[0] = x;
         for (int i = 1; i < kMtN; ++i) {
             x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
@@ -1157,6 +1158,8 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
+__global__ void k_set_seed(unsigned *seed, unsigned v) { *seed = v; }
+
 __global__ __launch_bounds__(64) void k_gather(const char *pool, long long stride, long long rb, const int *idx,
                                               char *out) {
     const int t = blockIdx.x;
@@ -1497,6 +1500,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     rc |= dalloc(b, &d.pb, (size_t)b->PS + kWave);
     rc |= dalloc(b, &d.sq, (size_t)b->PS + kWave);
     rc |= dalloc(b, &d.lp, (size_t)b->PS + 1 + kWave);
+    rc |= dalloc(b, &d.seed, 1);
     rc |= dalloc(b, &b->in_dev, (size_t)B * (2 + 3 * A));
     rc |= dalloc(b, &b->sel_dev, (size_t)3 * B);
     b->rb_words = (size_t)2 * B + 2 * (size_t)B * A + (size_t)MZ_F_COUNT * B * b->Wd;
@@ -1510,6 +1514,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     lp[0] = 1.0f;
     for (int k = 1; k < b->PS + 1; ++k) lp[k] = lp[k - 1] * lam;  // lam_pow chain (utils.cpp:25-27)
     if (hipMemcpy(d.lp, lp.data(), sizeof(float) * lp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d.seed, &seed, sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(d.hdr, 0, sizeof(TreeHdr) * B) != hipSuccess ||
         hipMemset(d.stats, 0, sizeof(long long) * B * MZ_S_COUNT) != hipSuccess ||
         hipMemset(d.err, 0, sizeof(int)) != hipSuccess) {
@@ -1698,8 +1703,19 @@ int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const f
 // include/mzdriver.h
 int mz_reseed(mz_batch *b, uint32_t seed) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    int rc = ensure_device(b);
+    if (rc) return rc;
     b->geo.seed = seed;
     b->prepared = false;
+    hipLaunchKernelGGL(k_set_seed, dim3(1), dim3(1), 0, b->stream, b->dev.seed, (unsigned)seed);
+    HIP_TRY(hipGetLastError());
+    return MZ_OK;
+}
+
+int mz_state_changed(mz_batch *b) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    b->rb_valid = b->rb_dev_valid = false;
+    b->prepared = true;
     return MZ_OK;
 }
 

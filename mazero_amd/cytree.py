@@ -220,7 +220,12 @@ class Tree_batch:
     def reseed(self, random_seed: int):
         """Same trees as a fresh Tree_batch(..., random_seed, ...) from the next prepare on
         (include/mzdriver.h, product library only)."""
+        self._sync_stream()
         check(self._lib, self._lib.mz_reseed(self._h, int(random_seed) & 0xFFFFFFFF), "reseed")
+
+    def state_changed(self):
+        """Drop host-side readback caches after replaying a captured graph of this handle's calls."""
+        check(self._lib, self._lib.mz_state_changed(self._h), "state_changed")
 
     # -- device readbacks (no host synchronisation) -------------------------------------------
     def get_roots_values_device(self, out=None):

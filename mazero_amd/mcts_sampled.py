@@ -98,6 +98,89 @@ def _dtype_code(t: torch.Tensor) -> int:
     raise TypeError(f"policy logits must be float32 or float16, got {t.dtype}")
 
 
+class _SearchLoop:
+    """Static device buffers of one search configuration and, after the first (eager) search, a
+    HIP graph of the whole simulation loop (prepare, S x [network, glue, fused tree kernel]).
+    Every input is copied into the static buffers before a run, and the tree seed lives in device
+    memory (mz_reseed), so replaying the graph is a new search."""
+
+    def __init__(self, tb, B, A, N, cur, hidden, dev):
+        self.tb, self.B, self.A, self.N, self.cur, self.dev = tb, B, A, N, cur, dev
+        self.root = torch.empty_like(hidden.reshape(B, -1))
+        self.rin = [torch.empty(n, dtype=torch.float32, device=dev) for n in (B, B, B * A, B * A, B * A)]
+        self.sel = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev),
+                    torch.empty(B, 1, dtype=torch.int32, device=dev))
+        self.joint = torch.empty(B, N, dtype=torch.int64, device=dev)
+        self.probs = torch.empty(B, A, dtype=torch.float32, device=dev)
+        self.beta = torch.empty(B, A, dtype=torch.float32, device=dev)
+        self.fac = torch.zeros(B, max(cur, 1), dtype=torch.int32, device=dev)
+        self.pool = None
+        self.leaf = None
+        self.graph = None
+        self.runs = 0
+
+    def load(self, hidden, root_arrays, factor):
+        self.root.copy_(hidden.reshape(self.B, -1))
+        for t, a in zip(self.rin, root_arrays):
+            t.copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+        if self.cur > 0:
+            self.fac.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(factor)[:, : self.cur], dtype=np.int32)))
+
+    def run(self, model, cfg, eps, tau):
+        """One search, mcts_sampled.py:106-172, all on the current stream."""
+        tb, B, A, N, cur = self.tb, self.B, self.A, self.N, self.cur
+        lib, h = tb._lib, tb._h
+        c2, c1, disc = cfg.pb_c_base, cfg.pb_c_init, cfg.discount
+        K, S = cfg.sampled_action_times, cfg.num_simulations
+        r = self.rin
+        tb.prepare(r[0], r[1], r[2], r[3], K, eps, r[4])
+        model.eval()
+        tb.batch_selection_device(c2, c1, disc, out=self.sel)
+        act = self.sel[2]
+        leaf = self.root  # simulation 0 selects a child of every root: its parent is the root (slot 0)
+        for s in range(S):
+            with torch.autocast("cuda", cache_enabled=False):
+                if cur + 1 < N:  # later agents' actions from the leaf policy, :136-145
+                    pred_logits, _ = model.prediction(leaf)
+                    pred_logits = pred_logits.contiguous()
+                    ptr, dt = C.c_void_p(pred_logits.data_ptr()), _dtype_code(pred_logits)
+                else:
+                    ptr, dt = None, MZ_DT_F32
+                check(lib, lib.mz_joint_action(h, ptr, dt, N, cur, C.c_void_p(self.fac.data_ptr()),
+                                               self.fac.shape[1], C.c_void_p(act.data_ptr()),
+                                               C.c_void_p(self.joint.data_ptr())), "joint_action")
+                next_h, reward, value, logits = SampledMCTS._recurrent(model, leaf, self.joint)  # :150-156
+            nh = next_h.reshape(B, -1)
+            if self.pool is None:
+                pdt = torch.promote_types(self.root.dtype, nh.dtype)
+                self.pool = torch.empty((S + 1, B, nh.shape[1]), dtype=pdt, device=self.dev)
+                self.leaf = torch.empty((B, nh.shape[1]), dtype=pdt, device=self.dev)
+            if s == 0:
+                self.pool[0].copy_(self.root)
+            self.pool[s + 1].copy_(nh)  # :164
+            logits = logits.contiguous()
+            check(lib, lib.mz_policy_glue(h, C.c_void_p(logits.data_ptr()), _dtype_code(logits),
+                                          logits.shape[1] * logits.shape[2], cur * A, float(tau),
+                                          C.c_void_p(self.probs.data_ptr()), C.c_void_p(self.beta.data_ptr())),
+                  "policy_glue")
+            r32 = reward.reshape(B).float()
+            v32 = value.reshape(B).float()
+            if s + 1 < S:
+                tb.expansion_backup_selection_device(s + 1, disc, K, r32, v32, self.probs, self.beta, c2, c1,
+                                                     out=self.sel, pool=self.pool, gather_out=self.leaf)
+                leaf = self.leaf
+            else:
+                tb.batch_expansion_and_backup(s + 1, disc, K, r32, v32, self.probs, self.beta)
+
+    def capture(self, model, cfg, eps, tau):
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.run(model, cfg, eps, tau)
+
+
+_LOOPS: dict = {}
+
+
 # One device arena per search geometry, kept across searches and across SampledMCTS instances (the
 # self-play worker makes a new SampledMCTS every environment step, selfplay_worker.py:187); a
 # search reseeds it instead of allocating a new tree batch as the reference does (:89).
@@ -107,10 +190,11 @@ _TREES: dict = {}
 class SampledMCTS:
     """mcts_sampled.py:29-32.  `lib` selects the tree library (default: the MI355X product)."""
 
-    def __init__(self, config, np_random: np.random.RandomState = None, *, lib=None):
+    def __init__(self, config, np_random: np.random.RandomState = None, *, lib=None, use_graph: bool = True):
         self.config = config
         self.np_random = np.random if np_random is None else np_random
         self._lib = lib
+        self.use_graph = use_graph
 
     # ---------------------------------------------------------------------------------------
     def root_inputs(self, network_output, current_agent_idx, legal_actions_lst, add_noise, sampled_tau):
@@ -193,60 +277,20 @@ class SampledMCTS:
                                                            sampled_tau)
         with torch.cuda.device(dev):
             tb = self._tree(B, seed, dev)
-            lib, h = tb._lib, tb._h
-            up = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (rr, rv, rp, rb, rn)]
-            tb.prepare(up[0], up[1], up[2], up[3], K, eps, up[4])
-
-            row = hidden.reshape(B, -1)
-            idx = torch.empty(B, dtype=torch.int32, device=dev)
-            idy = torch.empty(B, dtype=torch.int32, device=dev)
-            act = torch.empty(B, 1, dtype=torch.int32, device=dev)
-            sel = (idx, idy, act)
-            joint = torch.empty(B, N, dtype=torch.int64, device=dev)
-            probs = torch.empty(B, A, dtype=torch.float32, device=dev)
-            beta = torch.empty(B, A, dtype=torch.float32, device=dev)
-            fac = None
-            if cur > 0:
-                fac = torch.from_numpy(np.ascontiguousarray(np.asarray(factor)[:, :cur], dtype=np.int32)).to(dev)
-            pool = None
-            leaf = None
-
+            key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), tuple(hidden.shape), hidden.dtype)
+            st = _LOOPS.get(key)
+            if st is None:
+                st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev)
+            st.load(hidden, (rr, rv, rp, rb, rn), factor)
             with torch.no_grad():
-                model.eval()
-                tb.batch_selection_device(c2, c1, disc, out=sel)
-                leaf = row  # simulation 0 selects a child of every root: its parent is the root (slot 0)
-                for s in range(S):
-                    with torch.autocast("cuda"):
-                        if cur + 1 < N:  # later agents' actions from the leaf policy, :136-145
-                            pred_logits, _ = model.prediction(leaf)
-                            pred_logits = pred_logits.contiguous()
-                            ptr, dt = C.c_void_p(pred_logits.data_ptr()), _dtype_code(pred_logits)
-                        else:
-                            ptr, dt = None, MZ_DT_F32
-                        check(lib, lib.mz_joint_action(h, ptr, dt, N, cur,
-                                                       C.c_void_p(fac.data_ptr()) if fac is not None else None,
-                                                       cur, C.c_void_p(act.data_ptr()), C.c_void_p(joint.data_ptr())),
-                              "joint_action")
-                        next_h, reward, value, logits = self._recurrent(model, leaf, joint)  # :150-156
-                    nh = next_h.reshape(B, -1)
-                    if pool is None:
-                        pdt = torch.promote_types(row.dtype, nh.dtype)
-                        pool = torch.empty((S + 1, B, nh.shape[1]), dtype=pdt, device=dev)
-                        pool[0].copy_(row)
-                        leaf = torch.empty((B, nh.shape[1]), dtype=pdt, device=dev)
-                    pool[s + 1].copy_(nh)  # :164
-                    logits = logits.contiguous()
-                    check(lib, lib.mz_policy_glue(h, C.c_void_p(logits.data_ptr()), _dtype_code(logits),
-                                                  logits.shape[1] * logits.shape[2], cur * A, float(sampled_tau),
-                                                  C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr())),
-                          "policy_glue")
-                    r32 = reward.reshape(B).float()
-                    v32 = value.reshape(B).float()
-                    if s + 1 < S:
-                        tb.expansion_backup_selection_device(s + 1, disc, K, r32, v32, probs, beta, c2, c1,
-                                                             out=sel, pool=pool, gather_out=leaf)
-                    else:
-                        tb.batch_expansion_and_backup(s + 1, disc, K, r32, v32, probs, beta)
+                if not self.use_graph or st.runs == 0:
+                    st.run(model, cfg, eps, sampled_tau)  # eager (the first search also warms up)
+                else:
+                    if st.graph is None:
+                        st.capture(model, cfg, eps, sampled_tau)
+                    st.graph.replay()
+                    tb.state_changed()
+                st.runs += 1
 
             if _host_readback:  # :176-191 (one packed device->host copy)
                 return SearchOutput(

@@ -22,6 +22,7 @@ for s in $STEPS; do
     pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS} ;;
+    search) step bench_search 900 python bench_search.py ${SEARCH_ARGS} ;;
     stamps) MZ_STAMPS=1 step bench_stamps 600 python bench.py --no-cpu ${BENCH_ARGS} ;;
     prof)   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --no-cpu --steps 10 ${BENCH_ARGS} ;;
     pmc)    step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o bench -- python3 "$R/bench.py" --no-cpu --steps 5 ${BENCH_ARGS} &&

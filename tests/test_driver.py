@@ -294,3 +294,29 @@ def test_driver_device_outputs_and_reuse(port_lib):
             got = drv.batch_search(net, out, agent, factor, N, legal, device=dev, add_noise=True)
         _compare_outputs(got, exp)
     assert rs_o.randint(1 << 30) == rs_d.randint(1 << 30)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 5])
+def test_driver_graph_replay_matches_oracle(K, port_lib):
+    """Repeated searches of one configuration: the first runs eagerly, the second is captured into
+    a HIP graph and replayed, later ones replay it -- each with new roots, seed and factor."""
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, B, S, cur = 3, 9, 64, 20, 1
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=K)
+    net = make_net(N, A, seed=12, device=dev)
+    rs_o, rs_d = np.random.RandomState(5), np.random.RandomState(5)
+    oracle = OracleSampledMCTS(cfg, rs_o, port_lib)
+    drv = SampledMCTS(cfg, rs_d, use_graph=True)
+    for step in range(4):
+        out, legal = make_root_batch(net, B, 64, seed=100 + step, device=dev, legal_zero_frac=0.25)
+        factor = np.random.default_rng(step).integers(0, A, size=(B, cur)).astype(np.int32)
+        exp = oracle.batch_search(net, out, cur, factor, N, legal, device=dev, add_noise=True)
+        got = drv.batch_search(net, out, cur, factor, N, legal, device=dev, add_noise=True)
+        _compare_outputs(got, exp)
