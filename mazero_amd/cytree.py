@@ -95,6 +95,8 @@ class Tree_batch:
         check(lib, rc, "Tree_batch")
         self._keep = []  # host buffers that must outlive an enqueued call
         self._stream_ptr = None
+        # device backends follow torch's current stream on every call (oracle libraries are host-only)
+        self._on_device = torch is not None and lib.mz_backend() == b"hip-gfx950"
         self._maxdeg = None
 
     # -- lifetime ---------------------------------------------------------------------------
@@ -108,8 +110,10 @@ class Tree_batch:
             self._h = None
 
     def _sync_stream(self):
-        """Bind the handle to torch's current stream (device path only)."""
-        if torch is None:
+        """Bind the handle to torch's current stream, so its work is ordered with torch's (also
+        for host-buffer calls and readbacks: a graph replay or torch kernel on the current stream
+        must finish before the tree is read)."""
+        if not self._on_device:
             return
         s = torch.cuda.current_stream().cuda_stream
         if s != self._stream_ptr:
@@ -126,6 +130,7 @@ class Tree_batch:
             self._sync_stream()
             return [C.c_void_p(t.data_ptr()) for t in ts], MZ_MEM_DEVICE, ts
         hs = [_f32_host(a) for a in arrays]
+        self._sync_stream()
         return [h.ctypes.data_as(C.c_void_p) for h in hs], MZ_MEM_HOST, hs
 
     # -- search (cytree.pyx:21-91) --------------------------------------------------------------
@@ -142,6 +147,7 @@ class Tree_batch:
         idx = np.empty(B, np.int32)
         idy = np.empty(B, np.int32)
         act = np.empty(B * N, np.int32)
+        self._sync_stream()
         rc = self._lib.mz_select(
             self._h,
             float(pb_c_base),
@@ -225,6 +231,7 @@ class Tree_batch:
 
     def state_changed(self):
         """Drop host-side readback caches after replaying a captured graph of this handle's calls."""
+        self._sync_stream()
         check(self._lib, self._lib.mz_state_changed(self._h), "state_changed")
 
     # -- device readbacks (no host synchronisation) -------------------------------------------
@@ -266,18 +273,21 @@ class Tree_batch:
 
     # -- readbacks (cytree.pyx:93-241) ----------------------------------------------------------
     def get_roots_values(self):
+        self._sync_stream()
         out = np.empty(self.root_num, np.float32)
         check(self._lib, self._lib.mz_get_roots_values(self._h, out.ctypes.data_as(C.c_void_p), MZ_MEM_HOST),
               "get_roots_values")
         return out
 
     def get_roots_marginal_visit_count(self):
+        self._sync_stream()
         out = np.empty(self.root_num * self.agent_num * self.action_space_size, np.int32)
         check(self._lib, self._lib.mz_get_roots_marginal_visit_count(self._h, out.ctypes.data_as(C.c_void_p),
                                                                       MZ_MEM_HOST), "get_roots_marginal_visit_count")
         return out.reshape(self.root_num, self.agent_num, self.action_space_size)
 
     def get_roots_marginal_priors(self):
+        self._sync_stream()
         out = np.empty(self.root_num * self.agent_num * self.action_space_size, np.float32)
         check(self._lib, self._lib.mz_get_roots_marginal_priors(self._h, out.ctypes.data_as(C.c_void_p),
                                                                  MZ_MEM_HOST), "get_roots_marginal_priors")
@@ -298,6 +308,7 @@ class Tree_batch:
         width = W * N if name == "actions" else W
         out = np.zeros(B * width, dt)
         deg = np.zeros(B, np.int32)
+        self._sync_stream()
         rc = self._lib.mz_get_roots_sampled_padded(
             self._h, FIELDS[name], float(discount), out.ctypes.data_as(C.c_void_p), deg.ctypes.data_as(C.c_void_p),
             MZ_MEM_HOST,
@@ -348,10 +359,12 @@ class Tree_batch:
     # -- diagnostics ------------------------------------------------------------------------------
     def stats(self) -> dict:
         out = (C.c_int64 * _capi_stats_count())()
+        self._sync_stream()
         check(self._lib, self._lib.mz_get_stats(self._h, out), "stats")
         return dict(zip(_capi.STATS, list(out)))
 
     def synchronize(self):
+        self._sync_stream()
         check(self._lib, self._lib.mz_synchronize(self._h), "synchronize")
 
     def print(self):
