@@ -80,7 +80,7 @@ struct Geo {
     float one_minus_rho, delta;
     int reg_cap;  // value entries staged in LDS per back-propagation chunk
     // dynamic-LDS byte offsets of k_step
-    int oA, oB, oQ, oPP, oVs, oC, oPath, oFlag, oT, oPb, oSq, oLp, oRng, oBoot, oReg, lds;
+    int oA, oB, oQ, oPP, oVs, oC, oPath, oFlag, oT, oPb, oSq, oLp, oRng, oBoot, oReg, oX, lds;
 };
 
 struct Dev {
@@ -531,9 +531,8 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
 // 79-103) is recomputed as a reduction over the q of every visited non-root node -- exactly the
 // multiset's content.  Chunk 0's entries must already be in flight (stage_regions).
 // --------------------------------------------------------------------------------------------
-__device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float disc, TreeHdr &h,
-                       int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl,
-                       unsigned long long *ts) {
+__device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float reward, float disc,
+                       TreeHdr &h, int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl) {
     const int l = lane_id();
     const unsigned long long b0 = (MZ_STAMPS != 0) ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long b1 = 0, bw = 0;
@@ -543,7 +542,8 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         if (l == 0) s.boot[D] = b;
         for (int base = D; base >= 1; base -= kWave) {
             const int i = base - l;
-            const float r = (i >= 1) ? i2f(s.A[s.path[i].x].w) : 0.f;
+            // the leaf's reward is this simulation's input (the expansion wave stores it)
+            const float r = (i >= 1) ? ((i == D) ? reward : i2f(s.A[s.path[i].x].w)) : 0.f;
             const int n = base < kWave ? base : kWave;
             float mine = 0.f;
             int k = 0;
@@ -642,9 +642,13 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             }
             ent_w += nv - pos + 1;
             // node scalars
-            const int4 a4 = s.A[n];
+            // the leaf's record is being expanded by the other wave: it has children now (nc >= 1),
+            // its reward is this simulation's input, and its B record belongs to the expansion
+            const bool is_leaf = (i == D);
+            int4 a4 = s.A[n];
+            if (is_leaf) a4.w = f2i(reward);
             const int4 b4 = s.B[n];
-            const int nc = nc_of(b4.y);
+            const int nc = is_leaf ? 1 : nc_of(b4.y);
             const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
             const int4 na = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
             const int md = md_of(b4.y);
@@ -652,7 +656,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             const size_t gi = (size_t)t * g.P + n;
             d.A[gi] = na;
             d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
-            if (dep > md) {
+            if (dep > md && !is_leaf) {
                 const int4 nb4 = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
                 s.B[n] = nb4;
                 d.Bn[gi] = nb4;
@@ -677,8 +681,8 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         stl[MZ_S_CYC_BAK_WAIT] += (long long)bw;
         stl[MZ_S_CYC_BAK_NODES] += (long long)(b2 - b1 - bw);
     }
-    stamp(ts, 5);
-    // min/max over the q of visited non-root nodes
+    // min/max over the q of visited non-root nodes (`tot` = the node count before this
+    // simulation's expansion: the new children are unvisited, and the other wave writes them)
     float mn = INFINITY, mx = -INFINITY;
     int cv = 0;
     for (int base = 1; base < tot; base += kWave) {
@@ -928,58 +932,67 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // value entries the back-propagation needs, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
 template <bool EB, bool SEL>
-__global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
+__global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds s(smem, g);
     const int t = blockIdx.x;
-    const int l = threadIdx.x;
+    const int l = threadIdx.x & (kWave - 1);
+    // Two waves per tree.  Wave 0 expands the leaf, then selects and gathers; wave 1 back-propagates
+    // the path and recomputes the min/max normaliser at the same time: the expansion only creates
+    // new nodes and the leaf's structure fields, the back-propagation only updates existing path
+    // nodes (the leaf's visit / value / reward), so the two share no LDS or HBM word.
+    const int wv = uni((int)(threadIdx.x >> 6));
+    long long *xst = (long long *)(smem + g.oX);  // wave 1 -> wave 0: statistics, min/max, error
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
     const size_t nb = (size_t)t * g.P;
-    // ---- round 1: everything that does not depend on the tree header, issued together with it:
-    // tables, network outputs, the expansion's engine words (carried in the header), statistics,
-    // and the node records / path within the host's bounds a.ne / a.pe ----
-    if (SEL) {
-        if (g.use_table) {
-            for (int i0 = 0; i0 < g.TT; i0 += 4 * kWave)
-                if (i0 + 4 * l < g.TT) glds16(d.T + i0 + 4 * l, s.T + i0);
-        } else {
-            for (int i0 = 0; i0 < g.PS; i0 += kWave)
-                if (i0 + l < g.PS) glds4(d.pb + i0 + l, s.pb + i0);
-            for (int i0 = 0; i0 < 2 * g.PS; i0 += kWave)
-                if (i0 + l < 2 * g.PS) glds4((const int *)d.sq + i0 + l, (int *)s.sq + i0);
-        }
-    }
-    for (int i0 = 0; i0 < a.ne; i0 += kWave) {
-        if (i0 + l < a.ne) {
-            glds16(d.A + nb + i0 + l, s.A + i0);
-            glds16(d.Bn + nb + i0 + l, s.B + i0);
-            glds4(d.PP + nb + i0 + l, s.PP + i0);
-            if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
-        }
-    }
+    // ---- round 1: everything that does not depend on the tree header, issued with it --------
     float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
     unsigned w1r = 0u, w2r = 0u;
     const bool have_w = 2 * a.K <= kNxt;
-    if (EB) {
-        for (int i0 = 0; i0 < g.PS + 1; i0 += kWave)
-            if (i0 + l < g.PS + 1) glds4(d.lp + i0 + l, s.lp + i0);
-        for (int i0 = 0; i0 < 2 * a.pe; i0 += kWave)
-            if (i0 + l < 2 * a.pe) glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
-        const size_t ib = (size_t)t * g.A;
-        if (l < g.A) {
-            pol = a.policy[ib + l];
-            bet = a.beta[ib + l];
+    if (EB) r_in = a.reward[t];
+    if (EB) v_in = a.value[t];
+    if (wv == 0) {
+        if (SEL) {
+            if (g.use_table) {
+                for (int i0 = 0; i0 < g.TT; i0 += 4 * kWave)
+                    if (i0 + 4 * l < g.TT) glds16(d.T + i0 + 4 * l, s.T + i0);
+            } else {
+                for (int i0 = 0; i0 < g.PS; i0 += kWave)
+                    if (i0 + l < g.PS) glds4(d.pb + i0 + l, s.pb + i0);
+                for (int i0 = 0; i0 < 2 * g.PS; i0 += kWave)
+                    if (i0 + l < 2 * g.PS) glds4((const int *)d.sq + i0 + l, (int *)s.sq + i0);
+            }
         }
-        r_in = a.reward[t];
-        v_in = a.value[t];
-        if (have_w && l < a.K) {
-            w1r = d.hdr[t].nxt[2 * l];
-            w2r = d.hdr[t].nxt[2 * l + 1];
+        if (EB) {
+            const size_t ib = (size_t)t * g.A;
+            if (l < g.A) {
+                pol = a.policy[ib + l];
+                bet = a.beta[ib + l];
+            }
+            if (have_w && l < a.K) {
+                w1r = d.hdr[t].nxt[2 * l];
+                w2r = d.hdr[t].nxt[2 * l + 1];
+            }
+        }
+    } else {
+        for (int i0 = 0; i0 < a.ne; i0 += kWave) {
+            if (i0 + l < a.ne) {
+                glds16(d.A + nb + i0 + l, s.A + i0);
+                glds16(d.Bn + nb + i0 + l, s.B + i0);
+                glds4(d.PP + nb + i0 + l, s.PP + i0);
+                if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
+            }
+        }
+        if (EB) {
+            for (int i0 = 0; i0 < g.PS + 1; i0 += kWave)
+                if (i0 + l < g.PS + 1) glds4(d.lp + i0 + l, s.lp + i0);
+            for (int i0 = 0; i0 < 2 * a.pe; i0 += kWave)
+                if (i0 + l < 2 * a.pe) glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
         }
     }
     long long *st = d.stats + (size_t)t * MZ_S_COUNT;
-    const long long st_old = (l < MZ_S_COUNT) ? st[l] : 0;
+    const long long st_old = (wv == 0 && l < MZ_S_COUNT) ? st[l] : 0;
     TreeHdr h;
     {
         const TreeHdr *hp = d.hdr + t;
@@ -994,8 +1007,8 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     }
     wait_vm();
     stamp(ts, 1);
-    if (h.err) {
-        if (SEL && l == 0) {
+    if (h.err) {  // a dead tree stays dead (both waves see the same header)
+        if (SEL && wv == 0 && l == 0) {
             a.idx_x[t] = 0;
             a.idy[t] = t;
             a.act[t] = 0;
@@ -1009,7 +1022,7 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
 
     const int tot = h.tot;
     // slow path: the host bounds were too small (e.g. a graph replayed out of sequence)
-    if (tot > a.ne || (EB && h.D + 1 > a.pe)) {
+    if (wv == 1 && (tot > a.ne || (EB && h.D + 1 > a.pe))) {
         for (int i0 = a.ne; i0 < tot; i0 += kWave) {
             if (i0 + l < tot) {
                 glds16(d.A + nb + i0 + l, s.A + i0);
@@ -1026,54 +1039,95 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     }
     stamp(ts, 2);
 
-    // ---- round 2 (asynchronous): path-node scalars, the value entries back-propagation needs,
-    // the RNG window -- in flight while the leaf is expanded ----
+    // ---- round 2: wave 0 the RNG window (and the leaf's structure record); wave 1 the path
+    // nodes' value-set scalars and the value entries the back-propagation needs ------------
     int cnt0 = 0, n0 = 0, nv0 = 0, need0 = 0, off0 = 0;
-    if (EB) {
+    const int wbase = h.cursor;
+    int4 leaf_b = make_int4(0, 0, 0, 0);
+    if (wv == 0) {
+        for (int i0 = 0; i0 < kRngWin; i0 += kWave)
+            if (wbase + i0 + l < g.W) glds4(d.R + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
+        if (EB) leaf_b = d.Bn[nb + h.leaf];  // used after the expansion: no wait here
+        if (!EB || !have_w) wait_vm();  // the expansion reads its words from the window
+    } else if (EB) {
         for (int i0 = 0; i0 <= h.D; i0 += kWave)
             if (i0 + l <= h.D) glds16(d.C + nb + s.path[i0 + l].x, s.C + i0);
         cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
     }
-    const int wbase = h.cursor;
-    for (int i0 = 0; i0 < kRngWin; i0 += kWave)
-        if (wbase + i0 + l < g.W) glds4(d.R + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
-    if (!EB || !have_w) wait_vm();  // the expansion reads its words from the window
     stamp(ts, 3);
 
     int cursor = h.cursor;
     int ntot = tot;
+    if (EB) {
+        if (wv == 0) {
+            // ---- CTree::expand (cnode.cpp:224-295) of the leaf (expand_and_backprop, :452-469) ----
+            const int leaf = h.leaf;
+            long long st_new = 0;
+            const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err,
+                                       st_new, have_w, w1r, w2r, stl);
+            stl[MZ_S_EXPANDS] += 1;
+            stl[MZ_S_NEW_CHILDREN] += st_new;
+            if (!err && l == 0) {
+                // the leaf's structure: first child, children count, (maxdepth >= 0 after this
+                // simulation's back-propagation), pred_value, hidden_state_index_x
+                const int ly = uni(leaf_b.y);
+                const int md = md_of(ly) < 0 ? 0 : md_of(ly);
+                const int4 nbv = make_int4(tot, pack_y(nc, act_of(ly), md), f2i(v_in), a.hsx);
+                s.B[leaf] = nbv;
+                d.Bn[nb + leaf] = nbv;
+            }
+            stamp(ts, 4);
+        } else {
+            // ---- CTree::back_propagate (cnode.cpp:415-450) + the min/max normaliser ----
+            backup(g, d, s, t, h.D, tot, v_in, r_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl);
+            if (l < MZ_S_COUNT) {
+                long long mine = 0;
+#pragma unroll
+                for (int k = 0; k < MZ_S_COUNT; ++k)
+                    if (l == k) mine = stl[k];
+                xst[l] = mine;
+            }
+            if (l == 0) {
+                float *xf = (float *)(xst + MZ_S_COUNT);
+                int *xi = (int *)(xst + MZ_S_COUNT);
+                xf[0] = h.mm_min;
+                xf[1] = h.mm_max;
+                xi[2] = h.mm_cnt;
+                xi[3] = err;
+            }
+        }
+        __syncthreads();
+        if (wv == 1) {
+            wait_vm();  // nothing of wave 1 may be in flight when the block ends
+            return;
+        }
+        // wave 0: merge wave 1's results
+        {
+            const float *xf = (const float *)(xst + MZ_S_COUNT);
+            const int *xi = (const int *)(xst + MZ_S_COUNT);
+            h.mm_min = unif(xf[0]);
+            h.mm_max = unif(xf[1]);
+            h.mm_cnt = uni(xi[2]);
+            err |= uni(xi[3]);
+            const long long o = (l < MZ_S_COUNT) ? xst[l] : 0;
+#pragma unroll
+            for (int k = 0; k < MZ_S_COUNT; ++k) stl[k] += (k == l) ? o : 0;  // lane k owns counter k
+        }
+        if (!err) {
+            h.cursor = cursor;
+            h.tot = ntot;
+        }
+    } else {
+        __syncthreads();  // wave 1 staged the node records the selection reads
+        if (wv == 1) return;
+    }
+    stamp(ts, 5);
+    wait_vm();  // RNG window (and anything staged) has landed
+    stamp(ts, 6);
     bool gath_pending = false;
     int4 gv[4];
     char *gdst = nullptr;
     long long grb = 0;
-    if (EB) {
-        // ---- CTree::expand_and_backprop (cnode.cpp:452-469) ----
-        const int leaf = uni(s.path[h.D].x);
-        long long st_new = 0;
-        const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new,
-                                   have_w, w1r, w2r, stl);
-        stl[MZ_S_EXPANDS] += 1;
-        stl[MZ_S_NEW_CHILDREN] += st_new;
-        if (!err && l == 0) {
-            const int4 la = s.A[leaf];
-            const int4 lb = s.B[leaf];
-            const int4 na = make_int4(la.x, la.y, la.z, f2i(r_in));
-            const int4 nbv = make_int4(tot, pack_y(nc, act_of(lb.y), md_of(lb.y)), f2i(v_in), a.hsx);
-            s.A[leaf] = na;
-            s.B[leaf] = nbv;
-            d.A[nb + leaf] = na;
-            d.Bn[nb + leaf] = nbv;
-        }
-        wait_lds();
-        stamp(ts, 4);
-        if (!err) {
-            h.cursor = cursor;
-            h.tot = ntot;
-            backup(g, d, s, t, h.D, ntot, v_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl, ts);
-        }
-    }
-    wait_vm();  // RNG window (and anything staged) has landed
-    stamp(ts, 6);
     if (SEL && !err) {
         value_scores(g, s, h.tot, a.discount, h);
         // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
@@ -1144,7 +1198,8 @@ __global__ __launch_bounds__(64) void k_step(Geo g, Dev d, StepArgs a) {
     }
     stamp(ts, 9);
     if (MZ_STAMPS && EB && SEL && !err) {
-        // phases: header, stage1, stage2, expand, backup, minmax, select(+outputs), gather, epilogue
+        // wave 0's timeline: header, stage1, stage2, expand, wait for the back-propagation wave,
+        // value-set/RNG wait, select(+outputs), gather, epilogue
         for (int k = 0; k < 9; ++k) stl[MZ_S_CYC_HEADER + k] += (long long)(ts[k + 1] - ts[k]);
         stl[MZ_S_STAMPED] += 1;
     }
@@ -1356,11 +1411,11 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         a.pe = (int)(pe < g.PS ? pe : g.PS);
     }
     if (eb && sel)
-        hipLaunchKernelGGL((k_step<true, true>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<true, true>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
     else if (eb)
-        hipLaunchKernelGGL((k_step<true, false>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<true, false>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
     else
-        hipLaunchKernelGGL((k_step<false, true>), dim3(g.B), dim3(kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<false, true>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
     HIP_TRY(hipGetLastError());
     if (eb) {
         b->rb_valid = b->rb_dev_valid = false;
@@ -1476,6 +1531,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oRng = o; o += round16(4 * kRngWin);
     g.oBoot = o; o += round16(4 * g.PS);
     g.oReg = o; o += round16(8 * g.reg_cap);
+    g.oX = o; o += round16(8 * (MZ_S_COUNT + 2));
     g.lds = o;
     if (g.lds > 160 * 1024) {
         delete b;
