@@ -256,9 +256,6 @@ def main():
         if os.environ.get("MZ_STAMPS") == "1" and st.get("stamped", 0) > 0:
             # diagnostic build: average shader cycles per fused launch and tree, per phase
             roofline["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
-            roofline["select_level_cycles"] = {k[8:]: round(st[k] / max(1, st["path_edges"]), 1)
-                                               for k in st if k.startswith("cyc_sel_")}
-            roofline["phase_cycles"] = {k: v for k, v in roofline["phase_cycles"].items() if not k.startswith("sel_")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -75,22 +75,25 @@ enum mz_stat {
     MZ_S_ENTRIES_READ = 6,   /* value-set entries scanned by back-propagation              */
     MZ_S_ENTRIES_WRITTEN = 7,/* value-set entries written by back-propagation              */
     MZ_S_MINMAX_NODES = 8,   /* node q-values scanned for the min/max normaliser           */
-    /* Diagnostic builds only (compiled with MZ_STAMPS=1; zero otherwise): shader cycles spent in
-     * each phase of the fused simulation-step kernel, summed over trees and launches. */
-    MZ_S_CYC_HEADER = 9,     /* tree header load                                           */
-    MZ_S_CYC_STAGE1 = 10,    /* tables, path, network outputs -> LDS                       */
-    MZ_S_CYC_STAGE2 = 11,    /* node records, q, path scalars, RNG window -> LDS           */
+    /* Diagnostic builds only (compiled with MZ_STAMPS=1; zero otherwise): shader cycles of the
+     * fused simulation-step kernel, summed over trees and launches, read with s_memtime where the
+     * wave's instruction stream reaches each point (no forced waits).  Wave 0 (expansion,
+     * selection, gather): */
+    MZ_S_CYC_HEADER = 9,     /* round 1: header, tables, network outputs issued and waited   */
+    MZ_S_CYC_STAGE1 = 10,    /* slow-path check (host bounds too small)                    */
+    MZ_S_CYC_STAGE2 = 11,    /* round 2 issue: RNG window, the leaf's record               */
     MZ_S_CYC_EXPAND = 12,    /* leaf expansion                                             */
-    MZ_S_CYC_BACKUP = 13,    /* back-propagation (bootstrap + value sets)                  */
-    MZ_S_CYC_MINMAX = 14,    /* min/max normaliser                                         */
-    MZ_S_CYC_SELECT = 15,    /* selection walk                                             */
-    MZ_S_CYC_GATHER = 16,    /* hidden-state gather                                        */
-    MZ_S_CYC_EPILOGUE = 17,  /* header / path write-back                                   */
+    MZ_S_CYC_BACKUP = 13,    /* waiting for the back-propagation wave (barrier)            */
+    MZ_S_CYC_MINMAX = 14,    /* waiting for the RNG window                                 */
+    MZ_S_CYC_SELECT = 15,    /* value scores + selection walk                              */
+    MZ_S_CYC_GATHER = 16,    /* hidden-state gather loads                                  */
+    MZ_S_CYC_EPILOGUE = 17,  /* header write-back, gather stores, statistics               */
     MZ_S_STAMPED = 18,       /* stamped launches x trees                                   */
-    MZ_S_CYC_SEL_READ = 19,  /* selection levels: children records LDS read               */
-    MZ_S_CYC_SEL_SCORE = 20, /* selection levels: pUCT scores                              */
-    MZ_S_CYC_SEL_PICK = 21,  /* selection levels: arg-max scan, tie-break word             */
-    MZ_S_CYC_SEL_STEP = 22,  /* selection levels: descend                                  */
+    /* wave 1 (back-propagation): */
+    MZ_S_CYC_W1_ROUND1 = 19, /* round 1: node records, path, lambda powers issued and waited */
+    MZ_S_CYC_W1_STAGE2 = 20, /* round 2 issue: path-node value sets, value entries         */
+    MZ_S_CYC_W1_BACKUP = 21, /* back-propagation + min/max                                 */
+    MZ_S_CYC_W1_SYNC = 22,   /* wave 1's whole span, start to back-propagation done        */
     MZ_S_CYC_EXP_CDF = 23,   /* expansion: sampling distribution                           */
     MZ_S_CYC_EXP_DRAW = 24,  /* expansion: K draws                                         */
     MZ_S_CYC_EXP_NODES = 25, /* expansion: child creation                                  */

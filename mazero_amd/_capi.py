@@ -48,10 +48,10 @@ STATS = [
     "cyc_gather",
     "cyc_epilogue",
     "stamped",
-    "cyc_sel_read",
-    "cyc_sel_score",
-    "cyc_sel_pick",
-    "cyc_sel_step",
+    "cyc_w1_round1",
+    "cyc_w1_stage2",
+    "cyc_w1_backup",
+    "cyc_w1_sync",
     "cyc_exp_cdf",
     "cyc_exp_draw",
     "cyc_exp_nodes",

@@ -162,13 +162,10 @@ __device__ __forceinline__ void glds16(const void *src, void *lds_base) {
     __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)lds_base, 16, 0, 0);
 }
 
-// Phase stamp (diagnostic builds): drain this wave's memory traffic, then read the shader clock.
+// Phase stamp (diagnostic builds): the shader clock when the wave's instruction stream gets here
+// (no forced wait: loads in flight stay in flight).
 __device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
-    if constexpr (MZ_STAMPS != 0) {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        ts[i] = __builtin_amdgcn_s_memtime();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
+    if constexpr (MZ_STAMPS != 0) ts[i] = __builtin_amdgcn_s_memtime();
 }
 
 // Whole-wave reductions with DPP (no LDS round trips): xor-pairs, xor-quads, half-row and row
@@ -1079,7 +1076,15 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
             stamp(ts, 4);
         } else {
             // ---- CTree::back_propagate (cnode.cpp:415-450) + the min/max normaliser ----
+            stamp(ts, 4);
             backup(g, d, s, t, h.D, tot, v_in, r_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl);
+            stamp(ts, 5);
+            if (MZ_STAMPS && SEL) {
+                stl[MZ_S_CYC_W1_ROUND1] += (long long)(ts[1] - ts[0]);
+                stl[MZ_S_CYC_W1_STAGE2] += (long long)(ts[3] - ts[2]);
+                stl[MZ_S_CYC_W1_BACKUP] += (long long)(ts[5] - ts[4]);
+                stl[MZ_S_CYC_W1_SYNC] += (long long)(ts[5] - ts[0]);  // wave 1's whole span
+            }
             if (l < MZ_S_COUNT) {
                 long long mine = 0;
 #pragma unroll
