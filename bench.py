@@ -105,16 +105,19 @@ def main():
     searches = []
     for inp in host_inputs:
         tb = Tree_batch(B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"], root_offset=root_offset, lib=lib)
+        # one allocation per search for the network outputs ([S, B | B | B*A | B*A]) and one for
+        # the selection outputs: every distinct allocation a kernel touches costs a translation miss
+        net = dev_t(np.concatenate([inp.reward.reshape(S, -1), inp.value.reshape(S, -1), inp.policy.reshape(S, -1),
+                                    inp.beta.reshape(S, -1)], axis=1))
+        sel = torch.empty(3, B, dtype=torch.int32, device=dev)
         searches.append(dict(
             tb=tb,
             rr=dev_t(inp.root_reward), rv=dev_t(inp.root_value), rp=dev_t(inp.root_policy),
             rb=dev_t(inp.root_beta), rn=dev_t(inp.root_noise), eps=inp.noise_eps,
-            r=dev_t(inp.reward), v=dev_t(inp.value), p=dev_t(inp.policy), b=dev_t(inp.beta),
+            r=net[:, :B], v=net[:, B:2 * B], p=net[:, 2 * B:2 * B + B * A], b=net[:, 2 * B + B * A:],
             pool=torch.randn(S + 1, B, H, device=dev),
             leaf=torch.empty(B, H, device=dev),
-            idx=torch.empty(B, dtype=torch.int32, device=dev),
-            idy=torch.empty(B, dtype=torch.int32, device=dev),
-            act=torch.empty(B, 1, dtype=torch.int32, device=dev),
+            idx=sel[0], idy=sel[1], act=sel[2].view(B, 1),
             values=torch.empty(B, device=dev),
             visits=torch.empty(B, 1, A, dtype=torch.int32, device=dev),
         ))

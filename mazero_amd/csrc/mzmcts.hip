@@ -1396,14 +1396,23 @@ int ensure_tables(mz_batch *b, float c2, float c1) {
     return MZ_OK;
 }
 
-template <typename T>
-int dalloc(mz_batch *b, T **p, size_t count) {
-    void *q = nullptr;
-    HIP_TRY(hipMalloc(&q, count * sizeof(T) + 64));
-    b->allocs.push_back(q);
-    *p = (T *)q;
-    return MZ_OK;
-}
+// Sub-allocation of one device buffer (256-byte aligned arrays, in request order).
+struct ArenaPlan {
+    std::vector<std::pair<void **, size_t>> req;
+    size_t total = 0;
+    template <typename T>
+    void add(T **p, size_t count) {
+        req.emplace_back((void **)p, total);
+        total += (count * sizeof(T) + 64 + 255) & ~(size_t)255;
+    }
+    int allocate(mz_batch *b) {
+        void *q = nullptr;
+        HIP_TRY(hipMalloc(&q, total));
+        b->allocs.push_back(q);
+        for (auto &r : req) *r.first = (char *)q + r.second;
+        return MZ_OK;
+    }
+};
 
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
@@ -1545,27 +1554,35 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
-    rc |= dalloc(b, &d.A, nodes);
-    rc |= dalloc(b, &d.Bn, nodes);
-    rc |= dalloc(b, &d.C, nodes);
-    rc |= dalloc(b, &d.D, nodes);
-    rc |= dalloc(b, &d.Q, nodes);
-    rc |= dalloc(b, &d.PP, nodes);
-    rc |= dalloc(b, &d.T, (size_t)g.TT + 4 * kWave);
-    rc |= dalloc(b, &d.V, nodes * b->E);
-    rc |= dalloc(b, &d.R, (size_t)B * b->W);
-    rc |= dalloc(b, &d.hdr, (size_t)B);
-    rc |= dalloc(b, &d.path, (size_t)B * b->PS);
-    rc |= dalloc(b, &d.stats, (size_t)B * MZ_S_COUNT);
-    rc |= dalloc(b, &d.err, 1);
-    rc |= dalloc(b, &d.pb, (size_t)b->PS + kWave);
-    rc |= dalloc(b, &d.sq, (size_t)b->PS + kWave);
-    rc |= dalloc(b, &d.lp, (size_t)b->PS + 1 + kWave);
-    rc |= dalloc(b, &d.seed, 1);
-    rc |= dalloc(b, &b->in_dev, (size_t)B * (2 + 3 * A));
-    rc |= dalloc(b, &b->sel_dev, (size_t)3 * B);
-    b->rb_words = (size_t)2 * B + 2 * (size_t)B * A + (size_t)MZ_F_COUNT * B * b->Wd;
-    rc |= dalloc(b, &b->rb_dev, b->rb_words);
+    // One device allocation for every array of the handle, the arrays each launch touches first:
+    // every distinct allocation a kernel touches costs it a serialised address-translation miss
+    // (~270 cycles each, measured with scripts/ulat.hip), so the per-launch working set is packed
+    // into as few 2 MiB pages as possible.
+    {
+        ArenaPlan plan;
+        plan.add(&d.hdr, (size_t)B);
+        plan.add(&d.stats, (size_t)B * MZ_S_COUNT);
+        plan.add(&d.err, 1);
+        plan.add(&d.seed, 1);
+        plan.add(&d.lp, (size_t)b->PS + 1 + kWave);
+        plan.add(&d.T, (size_t)g.TT + 4 * kWave);
+        plan.add(&d.pb, (size_t)b->PS + kWave);
+        plan.add(&d.sq, (size_t)b->PS + kWave);
+        plan.add(&d.A, nodes);
+        plan.add(&d.Bn, nodes);
+        plan.add(&d.Q, nodes);
+        plan.add(&d.PP, nodes);
+        plan.add(&d.C, nodes);
+        plan.add(&d.path, (size_t)B * b->PS);
+        plan.add(&d.R, (size_t)B * b->W);
+        plan.add(&d.D, nodes);
+        plan.add(&b->sel_dev, (size_t)3 * B);
+        plan.add(&b->in_dev, (size_t)B * (2 + 3 * A));
+        b->rb_words = (size_t)2 * B + 2 * (size_t)B * A + (size_t)MZ_F_COUNT * B * b->Wd;
+        plan.add(&b->rb_dev, b->rb_words);
+        plan.add(&d.V, nodes * b->E);
+        rc = plan.allocate(b);
+    }
     if (rc) {
         std::string m = g_err;
         mz_destroy(b);

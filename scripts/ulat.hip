@@ -72,6 +72,22 @@ __global__ void k_dma(const int4 *src, int n16, unsigned long long *out) {
 
 __global__ void k_empty() {}
 
+// one load from each of `nbuf` separately allocated buffers, issued together (wave-uniform)
+struct Bufs {
+    int *p[16];
+};
+__global__ void k_multi(Bufs bufs, int nbuf, int stride_ints, unsigned long long *out) {
+    const int l = threadIdx.x;
+    unsigned long long t0 = memtime();
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < nbuf) acc += bufs.p[k][(blockIdx.x * stride_ints + l) & ((1 << 20) - 1)];
+    acc = __builtin_amdgcn_readfirstlane(acc);
+    unsigned long long t1 = memtime();
+    if (l == 0) out[blockIdx.x] = t1 - t0 + (acc == 12345);
+}
+
 int main() {
     const int B = 256;
     int *buf;
@@ -113,6 +129,24 @@ int main() {
         printf("global_load_lds x%2d (16 B/lane): median %.0f cycles\n", n16, med(B));
     }
 
+    {
+        // TLB / allocation spread: loads to 1, 4, 16 separately allocated 4 MiB buffers
+        std::vector<int *> bl(16);
+        for (auto &p : bl) {
+            CK(hipMalloc(&p, 4 << 20));
+            CK(hipMemset(p, 0, 4 << 20));
+        }
+        Bufs dbl;
+        for (int k = 0; k < 16; ++k) dbl.p[k] = bl[k];
+        for (int nbuf : {1, 4, 16}) {
+            for (int stride : {64, 4096}) {
+                hipLaunchKernelGGL(k_multi, dim3(B), dim3(64), 0, 0, dbl, nbuf, stride, out);
+                hipLaunchKernelGGL(k_multi, dim3(B), dim3(64), 0, 0, dbl, nbuf, stride, out);
+                CK(hipMemcpy(h.data(), out, B * 8, hipMemcpyDeviceToHost));
+                printf("loads from %2d buffers (wave stride %5d B): median %.0f cycles\n", nbuf, stride * 4, med(B));
+            }
+        }
+    }
     hipStream_t st;
     CK(hipStreamCreate(&st));
     hipEvent_t e0, e1;
