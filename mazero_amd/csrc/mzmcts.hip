@@ -1129,8 +1129,9 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     stamp(ts, 5);
     wait_vm();  // RNG window (and anything staged) has landed
     stamp(ts, 6);
+    // gathered row chunks (four named registers: an array here ends up in scratch memory)
     bool gath_pending = false;
-    int4 gv[4];
+    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
     char *gdst = nullptr;
     long long grb = 0;
     if (SEL && !err) {
@@ -1153,15 +1154,12 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
             const long long rb = a.row_bytes;
             if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0 && rb <= 4 * 16 * kWave) {
                 // up to 4 KiB per row: all loads in flight at once, stores after the header write-back
-                int4 v[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const long long o2 = (long long)(k * kWave + l) * 16;
-                    if (o2 < rb) v[k] = *(const int4 *)(src + o2);
-                }
+                const long long o = (long long)l * 16;
+                if (o < rb) gv0 = *(const int4 *)(src + o);
+                if (o + 1024 < rb) gv1 = *(const int4 *)(src + o + 1024);
+                if (o + 2048 < rb) gv2 = *(const int4 *)(src + o + 2048);
+                if (o + 3072 < rb) gv3 = *(const int4 *)(src + o + 3072);
                 gath_pending = true;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) gv[k] = v[k];
                 gdst = dst;
                 grb = rb;
             } else if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0) {
@@ -1195,11 +1193,11 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
         }
     }
     if (gath_pending) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const long long o2 = (long long)(k * kWave + l) * 16;
-            if (o2 < grb) *(int4 *)(gdst + o2) = gv[k];
-        }
+        const long long o = (long long)l * 16;
+        if (o < grb) *(int4 *)(gdst + o) = gv0;
+        if (o + 1024 < grb) *(int4 *)(gdst + o + 1024) = gv1;
+        if (o + 2048 < grb) *(int4 *)(gdst + o + 2048) = gv2;
+        if (o + 3072 < grb) *(int4 *)(gdst + o + 3072) = gv3;
     }
     stamp(ts, 9);
     if (MZ_STAMPS && EB && SEL && !err) {
