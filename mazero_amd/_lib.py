@@ -18,12 +18,15 @@ _lib = None
 
 
 def load() -> C.CDLL:
-    """The product library; MZ_STAMPS=1 in the environment selects the diagnostic build."""
+    """The product library; MZ_STAMPS=1 in the environment selects the diagnostic build
+    (MZ_LIB_OVERRIDE=<path> loads an experiment build of the same source instead)."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
         path = LIB_STAMPS if os.environ.get("MZ_STAMPS") == "1" else LIB
+        # experiment builds of the same source (scripts/, diagnostics only)
+        path = os.environ.get("MZ_LIB_OVERRIDE", path)
         try:
             import torch  # noqa: F401  (plumbing: share torch's HIP runtime)
         except Exception:

@@ -84,23 +84,28 @@ struct Geo {
 };
 
 struct Dev {
-    int4 *A;
-    int4 *Bn;
-    float *Q;
-    float *PP;
-    float4 *C;
-    float4 *D;
-    int2 *V;
-    unsigned *R;
-    TreeHdr *hdr;
-    int2 *path;  // [B][PS] {node, visit-at-selection}
-    long long *stats;
-    int *err;
-    float *T;    // [TT] pUCT coefficient table, index n*(n+1)/2 + v
-    float *pb;   // [PS] logf((n + c2 + 1)/c2) + c1
-    double *sq;  // [PS] sqrt(n)
-    float *lp;   // [PS+1] lambda^d as a float chain
-    unsigned *seed;  // [1] random_seed, read by k_prepare (device-side so captured graphs follow mz_reseed)
+    // Every array lives in one device allocation (the handle's arena): a base pointer plus
+    // 32-bit offsets in 256-byte units keeps the kernel arguments small (each pointer would take
+    // two SGPRs for the whole kernel).
+    char *base;
+    unsigned o_A, o_Bn, o_Q, o_PP, o_C, o_D, o_V, o_R, o_hdr, o_path, o_stats, o_err, o_T, o_pb, o_sq, o_lp, o_seed;
+    __host__ __device__ int4 *A() const { return (int4 *)(base + (size_t)o_A * 256); }  // [P] {visit, prior, value, reward}
+    __host__ __device__ int4 *Bn() const { return (int4 *)(base + (size_t)o_Bn * 256); }  // [P] {first_child, nc|act<<8|(maxdepth+1)<<16, pred_value, hsx}
+    __host__ __device__ float *Q() const { return (float *)(base + (size_t)o_Q * 256); }  // [P] q - parent.pred_value
+    __host__ __device__ float *PP() const { return (float *)(base + (size_t)o_PP * 256); }  // [P] parent pred_value
+    __host__ __device__ float4 *C() const { return (float4 *)(base + (size_t)o_C * 256); }  // [P] {weighted_sum, tot_weight, -, -}
+    __host__ __device__ float4 *D() const { return (float4 *)(base + (size_t)o_D * 256); }  // [P] {pred_prob, beta, beta_hat, -}
+    __host__ __device__ int2 *V() const { return (int2 *)(base + (size_t)o_V * 256); }  // [P][E] {depth, value}
+    __host__ __device__ unsigned *R() const { return (unsigned *)(base + (size_t)o_R * 256); }  // [W] mt19937 stream
+    __host__ __device__ TreeHdr *hdr() const { return (TreeHdr *)(base + (size_t)o_hdr * 256); }  // [B] tree header
+    __host__ __device__ int2 *path() const { return (int2 *)(base + (size_t)o_path * 256); }  // [B][PS] {node, visit-at-selection}
+    __host__ __device__ long long *stats() const { return (long long *)(base + (size_t)o_stats * 256); }  // [B][MZ_S_COUNT]
+    __host__ __device__ int *err() const { return (int *)(base + (size_t)o_err * 256); }  // [1]
+    __host__ __device__ float *T() const { return (float *)(base + (size_t)o_T * 256); }  // [TT] pUCT coefficient table, index n*(n+1)/2 + v
+    __host__ __device__ float *pb() const { return (float *)(base + (size_t)o_pb * 256); }  // [PS] logf((n + c2 + 1)/c2) + c1
+    __host__ __device__ double *sq() const { return (double *)(base + (size_t)o_sq * 256); }  // [PS] sqrt(n)
+    __host__ __device__ float *lp() const { return (float *)(base + (size_t)o_lp * 256); }  // [PS+1] lambda^d as a float chain
+    __host__ __device__ unsigned *seed() const { return (unsigned *)(base + (size_t)o_seed * 256); }  // [1] random_seed, read by k_prepare
 };
 
 struct StepArgs {
@@ -234,7 +239,7 @@ __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, co
         err |= kErrRng;
         return 0u;
     }
-    return d.R[(size_t)t * g.W + idx];
+    return d.R()[(size_t)t * g.W + idx];
 }
 
 // --------------------------------------------------------------------------------------------
@@ -330,12 +335,12 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
         const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
         const int4 b4 = make_int4(0, pack_y(0, l, -1), f2i(0.0f), -1);
         const size_t gi = (size_t)t * g.P + c;
-        d.A[gi] = a4;
-        d.Bn[gi] = b4;
-        d.C[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
-        d.D[gi] = make_float4(pol, bet, bh, 0.f);
-        d.Q[gi] = 0.f;
-        d.PP[gi] = pv;
+        d.A()[gi] = a4;
+        d.Bn()[gi] = b4;
+        d.C()[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d.D()[gi] = make_float4(pol, bet, bh, 0.f);
+        d.Q()[gi] = 0.f;
+        d.PP()[gi] = pv;
         if (s) {
             s->A[c] = a4;
             s->B[c] = b4;
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
     const int t = blockIdx.x;
     const int tid = threadIdx.x;
     if (tid == 0) {  // std::mt19937::seed: sequential by definition
-        unsigned x = d.seed[0] * 2333u + (unsigned)(g.root_offset + t);
+        unsigned x = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
         mt[0] = x;
         for (int i = 1; i < kMtN; ++i) {
             x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
@@ -410,7 +415,7 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
             if (k < kMtN) mt[k] = v;
             __syncthreads();
         }
-        unsigned *dst = d.R + (size_t)t * g.W + (size_t)blk * kMtN;
+        unsigned *dst = d.R() + (size_t)t * g.W + (size_t)blk * kMtN;
         for (int k = tid; k < kMtN; k += blockDim.x) {
             const unsigned z = mt_temper(mt[k]);
             dst[k] = z;
@@ -439,18 +444,18 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
         const size_t gi = (size_t)t * g.P;
         // first SubTreeValueSet::update: count 1, big and small empty -> insert into big
         float ws = 0.f, tw = 0.f;
-        const float lp0 = d.lp[0];
+        const float lp0 = d.lp()[0];
         if (value_lim(1, g.one_minus_rho) != 1) err |= kErrValueSet;
         tw += lp0;
         ws += lp0 * v;
         const float val = (nc > 0) ? ws / tw : 0.f;
-        d.A[gi] = make_int4(1, f2i(1.0f), f2i(val), f2i(r));
-        d.Bn[gi] = make_int4(1, pack_y(nc, 0, 0), f2i(v), 0);
-        d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
-        d.D[gi] = make_float4(1.f, 1.f, 1.f, 0.f);
-        d.Q[gi] = 0.f;
-        d.PP[gi] = 0.f;
-        d.V[gi * g.E] = make_int2(0, f2i(v));
+        d.A()[gi] = make_int4(1, f2i(1.0f), f2i(val), f2i(r));
+        d.Bn()[gi] = make_int4(1, pack_y(nc, 0, 0), f2i(v), 0);
+        d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
+        d.D()[gi] = make_float4(1.f, 1.f, 1.f, 0.f);
+        d.Q()[gi] = 0.f;
+        d.PP()[gi] = 0.f;
+        d.V()[gi * g.E] = make_int2(0, f2i(v));
         TreeHdr h;
         h.cursor = cursor;
         h.tot = tot;
@@ -461,12 +466,12 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
         h.mm_cnt = 0;
         h.leaf = 0;
         for (int j = 0; j < kNxt; ++j) h.nxt[j] = (cursor + j < kMtN) ? w0[cursor + j] : 0u;
-        d.hdr[t] = h;
-        d.path[(size_t)t * g.PS] = make_int2(0, 1);
-        long long *st = d.stats + (size_t)t * MZ_S_COUNT;
+        d.hdr()[t] = h;
+        d.path()[(size_t)t * g.PS] = make_int2(0, 1);
+        long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
         st[MZ_S_EXPANDS] += 1;
         st[MZ_S_NEW_CHILDREN] += st_new;
-        if (err) atomicOr(d.err, err);
+        if (err) atomicOr(d.err(), err);
     }
 }
 
@@ -505,7 +510,7 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
         if (l == j) off = acc;
         acc += vj;
     }
-    const int2 *gV = d.V + (size_t)t * g.P * g.E;
+    const int2 *gV = d.V() + (size_t)t * g.P * g.E;
     int *regdw = (int *)s.reg;
     const unsigned long long nm = ballot(l < cnt && need);
     for (unsigned long long m = nm; m; m &= m - 1ull) {
@@ -562,7 +567,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         wait_lds();
         b1 = __builtin_amdgcn_s_memtime();
     }
-    int2 *gV = d.V + (size_t)t * g.P * g.E;
+    int2 *gV = d.V() + (size_t)t * g.P * g.E;
     int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0;
     long long ent_r = 0, ent_w = 0;
     for (int i0 = 0; i0 <= D;) {
@@ -651,17 +656,17 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             const int md = md_of(b4.y);
             s.A[n] = na;
             const size_t gi = (size_t)t * g.P + n;
-            d.A[gi] = na;
-            d.C[gi] = make_float4(ws, tw, 0.f, 0.f);
+            d.A()[gi] = na;
+            d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
             if (dep > md && !is_leaf) {
                 const int4 nb4 = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
                 s.B[n] = nb4;
-                d.Bn[gi] = nb4;
+                d.Bn()[gi] = nb4;
             }
             if (i >= 1) {
                 const float q = (i2f(a4.w) + disc * val) - s.PP[n];  // get_qsa - father->pred_value
                 s.Q[n] = q;
-                d.Q[gi] = q;
+                d.Q()[gi] = q;
             }
         }
         wait_lds();
@@ -738,7 +743,7 @@ __device__ __forceinline__ unsigned select_word(const Geo &g, const Dev &d, cons
     if (o >= 0 && o < kWave) return (unsigned)rl((int)rw0, o);
     if (o >= kWave && o < 2 * kWave) return (unsigned)rl((int)rw1, o - kWave);
     if (cursor - lds_base >= 0 && cursor - lds_base < kRngWin) return (unsigned)uni((int)s.rng[cursor - lds_base]);
-    if (cursor < g.W) return (unsigned)uni((int)d.R[(size_t)t * g.W + cursor]);
+    if (cursor < g.W) return (unsigned)uni((int)d.R()[(size_t)t * g.W + cursor]);
     err |= kErrRng;
     return 0u;
 }
@@ -806,7 +811,7 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
         stl[MZ_S_PATH_EDGES] += D;
         stl[MZ_S_SCORED] += scored;
         wait_lds();
-        int2 *gp = d.path + (size_t)t * g.PS;
+        int2 *gp = d.path() + (size_t)t * g.PS;
         for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
         return;
     }
@@ -917,7 +922,7 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
     stl[MZ_S_SCORED] += scored;
     wait_lds();
     // publish the path {node, visit} for the next back-propagation
-    int2 *gp = d.path + (size_t)t * g.PS;
+    int2 *gp = d.path() + (size_t)t * g.PS;
     for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
 }
 
@@ -949,18 +954,24 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     const bool have_w = 2 * a.K <= kNxt;
     if (EB) r_in = a.reward[t];
     if (EB) v_in = a.value[t];
+#ifdef MZ_PROBE
+    unsigned long long pr0 = __builtin_amdgcn_s_memtime(), pr1 = 0, pr2 = 0;
+#endif
     if (wv == 0) {
         if (SEL) {
             if (g.use_table) {
                 for (int i0 = 0; i0 < g.TT; i0 += 4 * kWave)
-                    if (i0 + 4 * l < g.TT) glds16(d.T + i0 + 4 * l, s.T + i0);
+                    if (i0 + 4 * l < g.TT) glds16(d.T() + i0 + 4 * l, s.T + i0);
             } else {
                 for (int i0 = 0; i0 < g.PS; i0 += kWave)
-                    if (i0 + l < g.PS) glds4(d.pb + i0 + l, s.pb + i0);
+                    if (i0 + l < g.PS) glds4(d.pb() + i0 + l, s.pb + i0);
                 for (int i0 = 0; i0 < 2 * g.PS; i0 += kWave)
-                    if (i0 + l < 2 * g.PS) glds4((const int *)d.sq + i0 + l, (int *)s.sq + i0);
+                    if (i0 + l < 2 * g.PS) glds4((const int *)d.sq() + i0 + l, (int *)s.sq + i0);
             }
         }
+#ifdef MZ_PROBE
+        pr1 = __builtin_amdgcn_s_memtime();
+#endif
         if (EB) {
             const size_t ib = (size_t)t * g.A;
             if (l < g.A) {
@@ -968,31 +979,31 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
                 bet = a.beta[ib + l];
             }
             if (have_w && l < a.K) {
-                w1r = d.hdr[t].nxt[2 * l];
-                w2r = d.hdr[t].nxt[2 * l + 1];
+                w1r = d.hdr()[t].nxt[2 * l];
+                w2r = d.hdr()[t].nxt[2 * l + 1];
             }
         }
     } else {
         for (int i0 = 0; i0 < a.ne; i0 += kWave) {
             if (i0 + l < a.ne) {
-                glds16(d.A + nb + i0 + l, s.A + i0);
-                glds16(d.Bn + nb + i0 + l, s.B + i0);
-                glds4(d.PP + nb + i0 + l, s.PP + i0);
-                if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
+                glds16(d.A() + nb + i0 + l, s.A + i0);
+                glds16(d.Bn() + nb + i0 + l, s.B + i0);
+                glds4(d.PP() + nb + i0 + l, s.PP + i0);
+                if (EB) glds4(d.Q() + nb + i0 + l, s.Q + i0);
             }
         }
         if (EB) {
             for (int i0 = 0; i0 < g.PS + 1; i0 += kWave)
-                if (i0 + l < g.PS + 1) glds4(d.lp + i0 + l, s.lp + i0);
+                if (i0 + l < g.PS + 1) glds4(d.lp() + i0 + l, s.lp + i0);
             for (int i0 = 0; i0 < 2 * a.pe; i0 += kWave)
-                if (i0 + l < 2 * a.pe) glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
+                if (i0 + l < 2 * a.pe) glds4((const int *)(d.path() + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
         }
     }
-    long long *st = d.stats + (size_t)t * MZ_S_COUNT;
+    long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
     const long long st_old = (wv == 0 && l < MZ_S_COUNT) ? st[l] : 0;
     TreeHdr h;
     {
-        const TreeHdr *hp = d.hdr + t;
+        const TreeHdr *hp = d.hdr() + t;
         h.cursor = uni(hp->cursor);
         h.tot = uni(hp->tot);
         h.D = uni(hp->D);
@@ -1002,6 +1013,9 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
         h.mm_max = unif(hp->mm_max);
         h.leaf = uni(hp->leaf);
     }
+#ifdef MZ_PROBE
+    pr2 = __builtin_amdgcn_s_memtime();
+#endif
     wait_vm();
     stamp(ts, 1);
     if (h.err) {  // a dead tree stays dead (both waves see the same header)
@@ -1022,16 +1036,16 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     if (wv == 1 && (tot > a.ne || (EB && h.D + 1 > a.pe))) {
         for (int i0 = a.ne; i0 < tot; i0 += kWave) {
             if (i0 + l < tot) {
-                glds16(d.A + nb + i0 + l, s.A + i0);
-                glds16(d.Bn + nb + i0 + l, s.B + i0);
-                glds4(d.PP + nb + i0 + l, s.PP + i0);
-                if (EB) glds4(d.Q + nb + i0 + l, s.Q + i0);
+                glds16(d.A() + nb + i0 + l, s.A + i0);
+                glds16(d.Bn() + nb + i0 + l, s.B + i0);
+                glds4(d.PP() + nb + i0 + l, s.PP + i0);
+                if (EB) glds4(d.Q() + nb + i0 + l, s.Q + i0);
             }
         }
         if (EB)
             for (int i0 = 2 * a.pe; i0 < 2 * (h.D + 1); i0 += kWave)
                 if (i0 + l < 2 * (h.D + 1))
-                    glds4((const int *)(d.path + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
+                    glds4((const int *)(d.path() + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
         wait_vm();
     }
     stamp(ts, 2);
@@ -1043,12 +1057,12 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     int4 leaf_b = make_int4(0, 0, 0, 0);
     if (wv == 0) {
         for (int i0 = 0; i0 < kRngWin; i0 += kWave)
-            if (wbase + i0 + l < g.W) glds4(d.R + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
-        if (EB) leaf_b = d.Bn[nb + h.leaf];  // used after the expansion: no wait here
+            if (wbase + i0 + l < g.W) glds4(d.R() + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
+        if (EB) leaf_b = d.Bn()[nb + h.leaf];  // used after the expansion: no wait here
         if (!EB || !have_w) wait_vm();  // the expansion reads its words from the window
     } else if (EB) {
         for (int i0 = 0; i0 <= h.D; i0 += kWave)
-            if (i0 + l <= h.D) glds16(d.C + nb + s.path[i0 + l].x, s.C + i0);
+            if (i0 + l <= h.D) glds16(d.C() + nb + s.path[i0 + l].x, s.C + i0);
         cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
     }
     stamp(ts, 3);
@@ -1071,7 +1085,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
                 const int md = md_of(ly) < 0 ? 0 : md_of(ly);
                 const int4 nbv = make_int4(tot, pack_y(nc, act_of(ly), md), f2i(v_in), a.hsx);
                 s.B[leaf] = nbv;
-                d.Bn[nb + leaf] = nbv;
+                d.Bn()[nb + leaf] = nbv;
             }
             stamp(ts, 4);
         } else {
@@ -1179,7 +1193,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     // header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
     {
         int perr = 0;
-        TreeHdr *hp = d.hdr + t;
+        TreeHdr *hp = d.hdr() + t;
         if (l < kNxt) hp->nxt[l] = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
         if (l == 0) {
             hp->cursor = h.cursor;
@@ -1200,6 +1214,14 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
         if (o + 3072 < grb) *(int4 *)(gdst + o + 3072) = gv3;
     }
     stamp(ts, 9);
+#ifdef MZ_PROBE
+    if (EB && SEL && !err) {
+        stl[MZ_S_CYC_W1_ROUND1] = (long long)(pr0 - ts[0]);   // kernel start -> first loads issued
+        stl[MZ_S_CYC_W1_STAGE2] = (long long)(pr1 - pr0);     // T table issue
+        stl[MZ_S_CYC_W1_BACKUP] = (long long)(pr2 - pr1);     // inputs + header issue
+        stl[MZ_S_CYC_W1_SYNC] = (long long)(ts[1] - pr2);     // wait for round 1
+    }
+#endif
     if (MZ_STAMPS && EB && SEL && !err) {
         // wave 0's timeline: header, stage1, stage2, expand, wait for the back-propagation wave,
         // value-set/RNG wait, select(+outputs), gather, epilogue
@@ -1212,7 +1234,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     for (int k = 0; k < MZ_S_COUNT; ++k)
         if (l == k) mine = stl[k];
     if (l < MZ_S_COUNT) st[l] = st_old + mine;
-    if (l == 0 && err) atomicOr(d.err, err);
+    if (l == 0 && err) atomicOr(d.err(), err);
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
@@ -1242,8 +1264,8 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
     const int l = threadIdx.x;
     const int B = g.B, A = g.A;
     const size_t nb = (size_t)t * g.P;
-    const int4 ra = d.A[nb];
-    const int4 rbn = d.Bn[nb];
+    const int4 ra = d.A()[nb];
+    const int4 rbn = d.Bn()[nb];
     const int nc = nc_of(uni(rbn.y));
     const int fc = uni(rbn.x);
     float *fout = (float *)out;
@@ -1255,9 +1277,9 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
     float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
     if (has) {
-        ca = d.A[nb + fc + l];
-        cb = d.Bn[nb + fc + l];
-        cd = d.D[nb + fc + l];
+        ca = d.A()[nb + fc + l];
+        cb = d.Bn()[nb + fc + l];
+        cd = d.D()[nb + fc + l];
     }
     const int act = act_of(cb.y);
     // marginal visit counts / priors: lane a collects the child whose action is a
@@ -1357,7 +1379,7 @@ int ensure_device(mz_batch *b) {
 // Poll the handle's error word (synchronises the stream).
 int check_device_errors(mz_batch *b) {
     int e = 0;
-    HIP_TRY(hipMemcpyAsync(&e, b->dev.err, sizeof(int), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemcpyAsync(&e, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     if (e) return fail(MZ_ERR_RUNTIME, err_message(e));
     return MZ_OK;
@@ -1385,29 +1407,46 @@ int ensure_tables(mz_batch *b, float c2, float c1) {
             pbc = (float)((double)pbc * (sq[n] / (double)(v + 1)));
             T[(size_t)n * (n + 1) / 2 + v] = pbc;
         }
-    HIP_TRY(hipMemcpyAsync(b->dev.T, T.data(), sizeof(float) * T.size(), hipMemcpyHostToDevice, b->stream));
-    HIP_TRY(hipMemcpyAsync(b->dev.pb, pb.data(), sizeof(float) * b->PS, hipMemcpyHostToDevice, b->stream));
-    HIP_TRY(hipMemcpyAsync(b->dev.sq, sq.data(), sizeof(double) * b->PS, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->dev.T(), T.data(), sizeof(float) * T.size(), hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->dev.pb(), pb.data(), sizeof(float) * b->PS, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipMemcpyAsync(b->dev.sq(), sq.data(), sizeof(double) * b->PS, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->tbl_c2 = c2;
     b->tbl_c1 = c1;
     return MZ_OK;
 }
 
-// Sub-allocation of one device buffer (256-byte aligned arrays, in request order).
+// Sub-allocation of one device buffer (256-byte aligned arrays, in request order): Dev arrays get
+// offsets from Dev::base, host-side staging buffers get plain pointers.
 struct ArenaPlan {
-    std::vector<std::pair<void **, size_t>> req;
+    struct Req {
+        unsigned *off;
+        void **ptr;
+        size_t at;
+    };
+    std::vector<Req> req;
     size_t total = 0;
+    static size_t span(size_t bytes) { return (bytes + 64 + 255) & ~(size_t)255; }
     template <typename T>
-    void add(T **p, size_t count) {
-        req.emplace_back((void **)p, total);
-        total += (count * sizeof(T) + 64 + 255) & ~(size_t)255;
+    void dev(unsigned &off, size_t count) {
+        req.push_back({&off, nullptr, total});
+        total += span(count * sizeof(T));
     }
-    int allocate(mz_batch *b) {
+    template <typename T>
+    void ptr(T **p, size_t count) {
+        req.push_back({nullptr, (void **)p, total});
+        total += span(count * sizeof(T));
+    }
+    int allocate(mz_batch *b, Dev &d) {
+        if (total / 256 > 0xffffffffull) return fail(MZ_ERR_UNSUPPORTED, "device arena larger than 1 TiB");
         void *q = nullptr;
         HIP_TRY(hipMalloc(&q, total));
         b->allocs.push_back(q);
-        for (auto &r : req) *r.first = (char *)q + r.second;
+        d.base = (char *)q;
+        for (auto &r : req) {
+            if (r.off) *r.off = (unsigned)(r.at / 256);
+            else *r.ptr = (char *)q + r.at;
+        }
         return MZ_OK;
     }
 };
@@ -1558,28 +1597,28 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     // into as few 2 MiB pages as possible.
     {
         ArenaPlan plan;
-        plan.add(&d.hdr, (size_t)B);
-        plan.add(&d.stats, (size_t)B * MZ_S_COUNT);
-        plan.add(&d.err, 1);
-        plan.add(&d.seed, 1);
-        plan.add(&d.lp, (size_t)b->PS + 1 + kWave);
-        plan.add(&d.T, (size_t)g.TT + 4 * kWave);
-        plan.add(&d.pb, (size_t)b->PS + kWave);
-        plan.add(&d.sq, (size_t)b->PS + kWave);
-        plan.add(&d.A, nodes);
-        plan.add(&d.Bn, nodes);
-        plan.add(&d.Q, nodes);
-        plan.add(&d.PP, nodes);
-        plan.add(&d.C, nodes);
-        plan.add(&d.path, (size_t)B * b->PS);
-        plan.add(&d.R, (size_t)B * b->W);
-        plan.add(&d.D, nodes);
-        plan.add(&b->sel_dev, (size_t)3 * B);
-        plan.add(&b->in_dev, (size_t)B * (2 + 3 * A));
+        plan.dev<TreeHdr>(d.o_hdr, (size_t)B);
+        plan.dev<long long>(d.o_stats, (size_t)B * MZ_S_COUNT);
+        plan.dev<int>(d.o_err, 1);
+        plan.dev<unsigned>(d.o_seed, 1);
+        plan.dev<float>(d.o_lp, (size_t)b->PS + 1 + kWave);
+        plan.dev<float>(d.o_T, (size_t)g.TT + 4 * kWave);
+        plan.dev<float>(d.o_pb, (size_t)b->PS + kWave);
+        plan.dev<double>(d.o_sq, (size_t)b->PS + kWave);
+        plan.dev<int4>(d.o_A, nodes);
+        plan.dev<int4>(d.o_Bn, nodes);
+        plan.dev<float>(d.o_Q, nodes);
+        plan.dev<float>(d.o_PP, nodes);
+        plan.dev<float4>(d.o_C, nodes);
+        plan.dev<int2>(d.o_path, (size_t)B * b->PS);
+        plan.dev<unsigned>(d.o_R, (size_t)B * b->W);
+        plan.dev<float4>(d.o_D, nodes);
+        plan.ptr(&b->sel_dev, (size_t)3 * B);
+        plan.ptr(&b->in_dev, (size_t)B * (2 + 3 * A));
         b->rb_words = (size_t)2 * B + 2 * (size_t)B * A + (size_t)MZ_F_COUNT * B * b->Wd;
-        plan.add(&b->rb_dev, b->rb_words);
-        plan.add(&d.V, nodes * b->E);
-        rc = plan.allocate(b);
+        plan.ptr(&b->rb_dev, b->rb_words);
+        plan.dev<int2>(d.o_V, nodes * b->E);
+        rc = plan.allocate(b, d);
     }
     if (rc) {
         std::string m = g_err;
@@ -1589,11 +1628,11 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     std::vector<float> lp(b->PS + 1 + kWave, 0.f);
     lp[0] = 1.0f;
     for (int k = 1; k < b->PS + 1; ++k) lp[k] = lp[k - 1] * lam;  // lam_pow chain (utils.cpp:25-27)
-    if (hipMemcpy(d.lp, lp.data(), sizeof(float) * lp.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d.seed, &seed, sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(d.hdr, 0, sizeof(TreeHdr) * B) != hipSuccess ||
-        hipMemset(d.stats, 0, sizeof(long long) * B * MZ_S_COUNT) != hipSuccess ||
-        hipMemset(d.err, 0, sizeof(int)) != hipSuccess) {
+    if (hipMemcpy(d.lp(), lp.data(), sizeof(float) * lp.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d.seed(), &seed, sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d.hdr(), 0, sizeof(TreeHdr) * B) != hipSuccess ||
+        hipMemset(d.stats(), 0, sizeof(long long) * B * MZ_S_COUNT) != hipSuccess ||
+        hipMemset(d.err(), 0, sizeof(int)) != hipSuccess) {
         mz_destroy(b);
         return fail(MZ_ERR_DEVICE, "device initialisation failed");
     }
@@ -1659,7 +1698,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     }
     a.eps = noise_eps;
     a.K = K;
-    HIP_TRY(hipMemsetAsync(b->dev.err, 0, sizeof(int), b->stream));
+    HIP_TRY(hipMemsetAsync(b->dev.err(), 0, sizeof(int), b->stream));
     hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), 0, b->stream, b->geo, b->dev, a);
     HIP_TRY(hipGetLastError());
     b->rb_valid = b->rb_dev_valid = false;
@@ -1783,7 +1822,7 @@ int mz_reseed(mz_batch *b, uint32_t seed) {
     if (rc) return rc;
     b->geo.seed = seed;
     b->prepared = false;
-    hipLaunchKernelGGL(k_set_seed, dim3(1), dim3(1), 0, b->stream, b->dev.seed, (unsigned)seed);
+    hipLaunchKernelGGL(k_set_seed, dim3(1), dim3(1), 0, b->stream, b->dev.seed(), (unsigned)seed);
     HIP_TRY(hipGetLastError());
     return MZ_OK;
 }
@@ -1923,7 +1962,7 @@ int mz_get_stats(mz_batch *b, int64_t *out) {
     int rc = ensure_device(b);
     if (rc) return rc;
     std::vector<long long> st((size_t)b->B * MZ_S_COUNT);
-    HIP_TRY(hipMemcpyAsync(st.data(), b->dev.stats, sizeof(long long) * st.size(), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemcpyAsync(st.data(), b->dev.stats(), sizeof(long long) * st.size(), hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     for (int k = 0; k < MZ_S_COUNT; ++k) out[k] = 0;
     for (int t = 0; t < b->B; ++t)
@@ -1936,7 +1975,7 @@ int mz_print(mz_batch *b) {
     int rc = ensure_device(b);
     if (rc) return rc;
     std::vector<TreeHdr> h(b->B);
-    HIP_TRY(hipMemcpyAsync(h.data(), b->dev.hdr, sizeof(TreeHdr) * b->B, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemcpyAsync(h.data(), b->dev.hdr(), sizeof(TreeHdr) * b->B, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
     for (int t = 0; t < b->B; ++t)
         fprintf(stderr, "tree %d: nodes %d, rng cursor %d, last path length %d, err %d, minmax [%f, %f] (%d)\n", t,
