@@ -223,12 +223,81 @@ struct Lds {
     unsigned *rng;
     float *boot;
     int2 *reg;
-    __device__ Lds(unsigned char *s, const Geo &g)
-        : A((int4 *)(s + g.oA)), B((int4 *)(s + g.oB)), Q((float *)(s + g.oQ)), PP((float *)(s + g.oPP)),
-          Vs((float *)(s + g.oVs)), C((float4 *)(s + g.oC)), path((int2 *)(s + g.oPath)), flag((int *)(s + g.oFlag)),
-          T((float *)(s + g.oT)), pb((float *)(s + g.oPb)), sq((double *)(s + g.oSq)), lp((float *)(s + g.oLp)),
-          rng((unsigned *)(s + g.oRng)), boot((float *)(s + g.oBoot)), reg((int2 *)(s + g.oReg)) {}
 };
+
+// LDS layout of k_step.  Capacity classes NC = 64 .. 1024 (node pool K*(S+2) <= NC) have a
+// compile-time layout: every LDS address folds into an instruction's immediate offset and no
+// offset occupies an SGPR for the kernel's lifetime.  NC = 0 is the general layout, whose offsets
+// come from Geo (trees above 1024 nodes).  The compile-time classes compute pUCT coefficients from
+// the pb / sq tables (no staged pUCT table).
+constexpr int kRegCap = 2048;  // value entries staged per back-propagation chunk (static layouts)
+
+template <int NC>
+struct Layout {
+    static constexpr int r16(int x) { return (x + 15) & ~15; }
+    static constexpr int oA = 0;
+    static constexpr int oB = oA + r16(16 * NC);
+    static constexpr int oQ = oB + r16(16 * NC);
+    static constexpr int oPP = oQ + r16(4 * NC);
+    static constexpr int oVs = oPP + r16(4 * NC);
+    static constexpr int oC = oVs + r16(4 * NC);
+    static constexpr int oPath = oC + r16(16 * NC);
+    static constexpr int oFlag = oPath + r16(8 * NC);
+    static constexpr int oPb = oFlag + r16(4 * NC);
+    static constexpr int oSq = oPb + r16(4 * (NC + kWave));
+    static constexpr int oLp = oSq + r16(8 * (NC + kWave));
+    static constexpr int oRng = oLp + r16(4 * (NC + 1 + kWave));
+    static constexpr int oBoot = oRng + r16(4 * kRngWin);
+    static constexpr int oReg = oBoot + r16(4 * NC);
+    static constexpr int oX = oReg + r16(8 * kRegCap);
+    static constexpr int total = oX + r16(8 * (MZ_S_COUNT + 2));
+};
+
+template <int NC>
+__device__ __forceinline__ Lds make_lds(unsigned char *m, const Geo &g) {
+    Lds s;
+    if constexpr (NC > 0) {
+        using L = Layout<NC>;
+        s.A = (int4 *)(m + L::oA);
+        s.B = (int4 *)(m + L::oB);
+        s.Q = (float *)(m + L::oQ);
+        s.PP = (float *)(m + L::oPP);
+        s.Vs = (float *)(m + L::oVs);
+        s.C = (float4 *)(m + L::oC);
+        s.path = (int2 *)(m + L::oPath);
+        s.flag = (int *)(m + L::oFlag);
+        s.T = nullptr;
+        s.pb = (float *)(m + L::oPb);
+        s.sq = (double *)(m + L::oSq);
+        s.lp = (float *)(m + L::oLp);
+        s.rng = (unsigned *)(m + L::oRng);
+        s.boot = (float *)(m + L::oBoot);
+        s.reg = (int2 *)(m + L::oReg);
+    } else {
+        s.A = (int4 *)(m + g.oA);
+        s.B = (int4 *)(m + g.oB);
+        s.Q = (float *)(m + g.oQ);
+        s.PP = (float *)(m + g.oPP);
+        s.Vs = (float *)(m + g.oVs);
+        s.C = (float4 *)(m + g.oC);
+        s.path = (int2 *)(m + g.oPath);
+        s.flag = (int *)(m + g.oFlag);
+        s.T = (float *)(m + g.oT);
+        s.pb = (float *)(m + g.oPb);
+        s.sq = (double *)(m + g.oSq);
+        s.lp = (float *)(m + g.oLp);
+        s.rng = (unsigned *)(m + g.oRng);
+        s.boot = (float *)(m + g.oBoot);
+        s.reg = (int2 *)(m + g.oReg);
+    }
+    return s;
+}
+
+template <int NC>
+__device__ __forceinline__ long long *lds_xchg(unsigned char *m, const Geo &g) {
+    if constexpr (NC > 0) return (long long *)(m + Layout<NC>::oX);
+    return (long long *)(m + g.oX);
+}
 
 // RNG word `idx` (per lane) of tree t: LDS window [wbase, wbase+kRngWin) or HBM.
 __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, const unsigned *win, int wbase, int t,
@@ -933,10 +1002,10 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // records, q / parent values, RNG window -- issued before one wait; (3) path-node scalars and the
 // value entries the back-propagation needs, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
-template <bool EB, bool SEL>
+template <bool EB, bool SEL, int NC>
 __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    Lds s(smem, g);
+    Lds s = make_lds<NC>(smem, g);
     const int t = blockIdx.x;
     const int l = threadIdx.x & (kWave - 1);
     // Two waves per tree.  Wave 0 expands the leaf, then selects and gathers; wave 1 back-propagates
@@ -944,7 +1013,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     // new nodes and the leaf's structure fields, the back-propagation only updates existing path
     // nodes (the leaf's visit / value / reward), so the two share no LDS or HBM word.
     const int wv = uni((int)(threadIdx.x >> 6));
-    long long *xst = (long long *)(smem + g.oX);  // wave 1 -> wave 0: statistics, min/max, error
+    long long *xst = lds_xchg<NC>(smem, g);  // wave 1 -> wave 0: statistics, min/max, error
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
     const size_t nb = (size_t)t * g.P;
@@ -959,7 +1028,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
 #endif
     if (wv == 0) {
         if (SEL) {
-            if (g.use_table) {
+            if (NC == 0 && g.use_table) {
                 for (int i0 = 0; i0 < g.TT; i0 += 4 * kWave)
                     if (i0 + 4 * l < g.TT) glds16(d.T() + i0 + 4 * l, s.T + i0);
             } else {
@@ -1340,6 +1409,7 @@ struct mz_batch {
     float tbl_c2 = NAN, tbl_c1 = NAN;
     bool prepared = false;
     long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
+    int nc = 0;                // k_step layout class (0 = layout from Geo)
 };
 
 namespace {
@@ -1451,6 +1521,24 @@ struct ArenaPlan {
     }
 };
 
+template <int NC>
+void launch_nc(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
+    const Geo &g = b->geo;
+    if (eb && sel)
+        hipLaunchKernelGGL((k_step<true, true, NC>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+    else if (eb)
+        hipLaunchKernelGGL((k_step<true, false, NC>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+    else
+        hipLaunchKernelGGL((k_step<false, true, NC>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+}
+
+template <int NC>
+void set_lds_limit(int lds) {
+    (void)hipFuncSetAttribute((const void *)k_step<true, true, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void *)k_step<true, false, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void *)k_step<false, true, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
     // tot <= 1 + K * expansions and depth <= expansions: the kernel stages that much without
@@ -1461,12 +1549,14 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         const long long pe = b->expansions + 1;
         a.pe = (int)(pe < g.PS ? pe : g.PS);
     }
-    if (eb && sel)
-        hipLaunchKernelGGL((k_step<true, true>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
-    else if (eb)
-        hipLaunchKernelGGL((k_step<true, false>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
-    else
-        hipLaunchKernelGGL((k_step<false, true>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+    switch (b->nc) {
+        case 64: launch_nc<64>(b, eb, sel, a); break;
+        case 128: launch_nc<128>(b, eb, sel, a); break;
+        case 256: launch_nc<256>(b, eb, sel, a); break;
+        case 512: launch_nc<512>(b, eb, sel, a); break;
+        case 1024: launch_nc<1024>(b, eb, sel, a); break;
+        default: launch_nc<0>(b, eb, sel, a); break;
+    }
     HIP_TRY(hipGetLastError());
     if (eb) {
         b->rb_valid = b->rb_dev_valid = false;
@@ -1566,6 +1656,9 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     }
     g.TT = ((g.PS * (g.PS + 1) / 2) + 3) & ~3;
     g.use_table = (4 * g.TT <= kTableLdsMax) ? 1 : 0;
+#ifdef MZ_NO_TABLE
+    g.use_table = 0;
+#endif
     int o = 0;
     g.oA = o; o += round16(16 * g.P);
     g.oB = o; o += round16(16 * g.P);
@@ -1584,6 +1677,27 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oReg = o; o += round16(8 * g.reg_cap);
     g.oX = o; o += round16(8 * (MZ_S_COUNT + 2));
     g.lds = o;
+    // compile-time layout class (pb / sq pUCT tables, value-entry chunks of kRegCap)
+    b->nc = 0;
+    for (int nc : {64, 128, 256, 512, 1024})
+        if (b->P <= nc) {
+            b->nc = nc;
+            break;
+        }
+#ifdef MZ_DYNAMIC_LAYOUT
+    b->nc = 0;
+#endif
+    if (b->nc) {
+        g.use_table = 0;
+        if (g.reg_cap > kRegCap) g.reg_cap = kRegCap;
+        switch (b->nc) {
+            case 64: g.lds = Layout<64>::total; break;
+            case 128: g.lds = Layout<128>::total; break;
+            case 256: g.lds = Layout<256>::total; break;
+            case 512: g.lds = Layout<512>::total; break;
+            default: g.lds = Layout<1024>::total; break;
+        }
+    }
     if (g.lds > 160 * 1024) {
         delete b;
         return fail(MZ_ERR_UNSUPPORTED, "tree too large for the LDS-resident kernels (K*(S+2) nodes)");
@@ -1637,9 +1751,14 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         return fail(MZ_ERR_DEVICE, "device initialisation failed");
     }
     if (g.lds > 64 * 1024) {
-        (void)hipFuncSetAttribute((const void *)k_step<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
-        (void)hipFuncSetAttribute((const void *)k_step<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
-        (void)hipFuncSetAttribute((const void *)k_step<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds);
+        switch (b->nc) {
+            case 64: set_lds_limit<64>(g.lds); break;
+            case 128: set_lds_limit<128>(g.lds); break;
+            case 256: set_lds_limit<256>(g.lds); break;
+            case 512: set_lds_limit<512>(g.lds); break;
+            case 1024: set_lds_limit<1024>(g.lds); break;
+            default: set_lds_limit<0>(g.lds); break;
+        }
     }
     *out = b;
     return MZ_OK;

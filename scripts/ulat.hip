@@ -72,6 +72,22 @@ __global__ void k_dma(const int4 *src, int n16, unsigned long long *out) {
 
 __global__ void k_empty() {}
 
+// instruction-fetch cost: 2048 straight-line VALU ops vs the same count in a 16-op loop
+__global__ void k_straight(unsigned long long *out) {
+    unsigned long long t0 = memtime();
+    float x = threadIdx.x;
+    asm volatile(".rept 2048\n v_add_f32 %0, 1.0, %0\n .endr" : "+v"(x));
+    unsigned long long t1 = memtime();
+    if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0 + (x == -1.f);
+}
+__global__ void k_looped(unsigned long long *out) {
+    unsigned long long t0 = memtime();
+    float x = threadIdx.x;
+    for (int i = 0; i < 128; ++i) asm volatile(".rept 16\n v_add_f32 %0, 1.0, %0\n .endr" : "+v"(x));
+    unsigned long long t1 = memtime();
+    if (threadIdx.x == 0) out[blockIdx.x] = t1 - t0 + (x == -1.f);
+}
+
 // one load from each of `nbuf` separately allocated buffers, issued together (wave-uniform)
 struct Bufs {
     int *p[16];
@@ -146,6 +162,14 @@ int main() {
                 printf("loads from %2d buffers (wave stride %5d B): median %.0f cycles\n", nbuf, stride * 4, med(B));
             }
         }
+    }
+    for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(k_straight, dim3(B), dim3(64), 0, 0, out);
+        CK(hipMemcpy(h.data(), out, B * 8, hipMemcpyDeviceToHost));
+        const double a = med(B);
+        hipLaunchKernelGGL(k_looped, dim3(B), dim3(64), 0, 0, out);
+        CK(hipMemcpy(h.data(), out, B * 8, hipMemcpyDeviceToHost));
+        printf("2048 VALU ops: straight-line %.0f cycles, looped %.0f cycles\n", a, med(B));
     }
     hipStream_t st;
     CK(hipStreamCreate(&st));

@@ -126,6 +126,7 @@ BIG = [
     ("3s5z_k5", 512, 15, 5, 100, 0.3),
     ("27m_k1", 256, 36, 1, 200, 0.0),
     ("27m_k5", 256, 36, 5, 200, 0.0),
+    ("27m_k8_general_layout", 64, 36, 8, 200, 0.0),  # 1616-node pool: LDS layout from Geo (class 0)
 ]
 
 
