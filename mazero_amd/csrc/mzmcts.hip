@@ -617,20 +617,17 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
             const float r = (i >= 1) ? ((i == D) ? reward : i2f(s.A[s.path[i].x].w)) : 0.f;
             const int n = base < kWave ? base : kWave;
             float mine = 0.f;
-            // fully unrolled: constant readlane indices let the compiler issue every broadcast ahead
-            // of the chain, so each step costs one dependent multiply-add pair (no FMA: the
-            // reference rounds the product)
+            int k = 0;
+            for (; k + 8 <= n; k += 8) {  // blocks of 8 fully unrolled steps (see expand_node)
 #pragma unroll
-            for (int kb = 0; kb < kWave; kb += 8) {
-                if (kb < n) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        if (kb + j < n) {
-                            b = rlf(r, kb + j) + disc * b;
-                            mine = (l == kb + j) ? b : mine;
-                        }
-                    }
+                for (int j = 0; j < 8; ++j) {
+                    b = rlf(r, k + j) + disc * b;
+                    mine = (l == k + j) ? b : mine;
                 }
+            }
+            for (; k < n; ++k) {
+                b = rlf(r, k) + disc * b;
+                mine = (l == k) ? b : mine;
             }
             if (l < n) s.boot[base - l - 1] = mine;
         }
