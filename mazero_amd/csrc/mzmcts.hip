@@ -1023,6 +1023,27 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     const bool have_w = 2 * a.K <= kNxt;
     if (EB) r_in = a.reward[t];
     if (EB) v_in = a.value[t];
+    // gathered row chunks (four named registers: an array here ends up in scratch memory).  A K = 1
+    // tree is a chain: the next leaf is the child this simulation's expansion creates, whose
+    // parent has hidden_state_index_x = a.hsx, so its row is fetched now and checked after the
+    // selection.
+    bool gath_pending = false;
+    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+    char *gdst = nullptr;
+    long long grb = 0;
+    const bool g_fast = SEL && a.pool &&
+                        (((a.row_bytes | a.pool_stride | (long long)(uintptr_t)a.pool |
+                           (long long)(uintptr_t)a.gather_out) & 15) == 0) &&
+                        a.row_bytes <= 4 * 16 * kWave;
+    const bool g_pre = EB && g_fast && g.K == 1;
+    if (wv == 0 && g_pre) {
+        const char *src = a.pool + (long long)a.hsx * a.pool_stride + (long long)t * a.row_bytes;
+        const long long rb = a.row_bytes, o = (long long)l * 16;
+        if (o < rb) gv0 = *(const int4 *)(src + o);
+        if (o + 1024 < rb) gv1 = *(const int4 *)(src + o + 1024);
+        if (o + 2048 < rb) gv2 = *(const int4 *)(src + o + 2048);
+        if (o + 3072 < rb) gv3 = *(const int4 *)(src + o + 3072);
+    }
 #ifdef MZ_PROBE
     unsigned long long pr0 = __builtin_amdgcn_s_memtime(), pr1 = 0, pr2 = 0;
 #endif
@@ -1212,11 +1233,6 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     stamp(ts, 5);
     wait_vm();  // RNG window (and anything staged) has landed
     stamp(ts, 6);
-    // gathered row chunks (four named registers: an array here ends up in scratch memory)
-    bool gath_pending = false;
-    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
-    char *gdst = nullptr;
-    long long grb = 0;
     if (SEL && !err) {
         value_scores(g, s, h.tot, a.discount, h);
         // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
@@ -1235,7 +1251,11 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
             const char *src = a.pool + (long long)idx * a.pool_stride + (long long)t * a.row_bytes;
             char *dst = a.gather_out + (long long)t * a.row_bytes;
             const long long rb = a.row_bytes;
-            if (((rb | (long long)(uintptr_t)src | (long long)(uintptr_t)dst) & 15) == 0 && rb <= 4 * 16 * kWave) {
+            if (g_pre && idx == a.hsx) {  // prefetched in round 1
+                gath_pending = true;
+                gdst = dst;
+                grb = rb;
+            } else if (g_fast) {
                 // up to 4 KiB per row: all loads in flight at once, stores after the header write-back
                 const long long o = (long long)l * 16;
                 if (o < rb) gv0 = *(const int4 *)(src + o);
