@@ -1036,14 +1036,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
                            (long long)(uintptr_t)a.gather_out) & 15) == 0) &&
                         a.row_bytes <= 4 * 16 * kWave;
     const bool g_pre = EB && g_fast && g.K == 1;
-    if (wv == 0 && g_pre) {
-        const char *src = a.pool + (long long)a.hsx * a.pool_stride + (long long)t * a.row_bytes;
-        const long long rb = a.row_bytes, o = (long long)l * 16;
-        if (o < rb) gv0 = *(const int4 *)(src + o);
-        if (o + 1024 < rb) gv1 = *(const int4 *)(src + o + 1024);
-        if (o + 2048 < rb) gv2 = *(const int4 *)(src + o + 2048);
-        if (o + 3072 < rb) gv3 = *(const int4 *)(src + o + 3072);
-    }
+
 #ifdef MZ_PROBE
     unsigned long long pr0 = __builtin_amdgcn_s_memtime(), pr1 = 0, pr2 = 0;
 #endif
@@ -1106,7 +1099,19 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
 #ifdef MZ_PROBE
     pr2 = __builtin_amdgcn_s_memtime();
 #endif
-    wait_vm();
+    if (wv == 0 && g_pre) {
+        // issued last and always exactly four loads (offsets clamped into the row), so the
+        // round-1 wait below can leave them in flight: the row is needed only at the very end
+        const char *src = a.pool + (long long)a.hsx * a.pool_stride + (long long)t * a.row_bytes;
+        const long long last = a.row_bytes - 16, o = (long long)l * 16;
+        gv0 = *(const int4 *)(src + (o < last ? o : last));
+        gv1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
+        gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
+        gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+        wait_vm();
+    }
     stamp(ts, 1);
     if (h.err) {  // a dead tree stays dead (both waves see the same header)
         if (SEL && wv == 0 && l == 0) {
