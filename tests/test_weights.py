@@ -1,0 +1,138 @@
+"""Weight broadcast for process-per-GPU self-play (mazero_amd.weights) over gloo, world size 2.
+
+The reference polls a Ray actor for a new checkpoint before each environment step
+(selfplay_worker.py:371-375). Here rank 0 publishes a model index and every rank calls sync()
+before the step. Checked here:
+- the weights arrive bit-identical in the live model, whose parameters are views of the flat
+  buffers;
+- an unchanged index moves no weights;
+- the model still trains and infers afterwards.
+The GPU variant (RCCL) runs the same code in tests/test_gpu_parity.py.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from mazero_amd.nets import make_net
+    from mazero_amd.weights import WeightBroadcaster
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    net = make_net(3, 9, seed=100 + rank)  # different weights on every rank
+    wb = WeightBroadcaster(net, src=0)
+    checks = []
+    # nothing published yet: index -1 everywhere, no weight traffic
+    checks.append(wb.sync() == -1)
+    if rank == 0:
+        with torch.no_grad():
+            for p in net.parameters():
+                p.add_(0.5)
+        wb.publish(7)
+    checks.append(wb.sync() == 7)
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    ref = [None] * world
+    dist.all_gather_object(ref, sd)
+    checks.append(all(torch.equal(ref[0][k], ref[1][k]) for k in sd))
+    # parameters are still views of the flat buffer (a second broadcast lands in the live model)
+    flat = wb.flat.tensors()[0]
+    p0 = next(net.parameters())
+    checks.append(p0.data_ptr() >= flat.data_ptr() and p0.data_ptr() < flat.data_ptr() + flat.numel() * flat.element_size())
+    if rank == 0:
+        with torch.no_grad():
+            p0.mul_(2.0)
+    # same index: no weights move (rank 1 keeps its copy)
+    wb.sync()
+    checks.append((rank == 0) or torch.equal(p0, ref[1][next(iter(sd))]))
+    # the model still runs and trains
+    out = net.prediction(torch.randn(4, 3 * 128))[0]
+    out.sum().backward()
+    checks.append(all(p.grad is not None for p in net.policy_head.parameters()))
+    q.put((rank, checks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_flat_weights_preserve_model():
+    from mazero_amd.nets import make_net
+    from mazero_amd.weights import FlatWeights
+
+    net = make_net(3, 9, seed=1)
+    x = torch.randn(5, 3 * 128)
+    before = net.prediction(x)[0].detach().clone()
+    fw = FlatWeights(net)
+    assert fw.numel == sum(p.numel() for p in net.parameters()) + sum(
+        b.numel() for b in net.buffers() if b.is_floating_point())
+    assert torch.equal(net.prediction(x)[0].detach(), before)
+
+
+@pytest.mark.timeout(300)
+def test_gloo_two_ranks_broadcast():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: [True] * 6, 1: [True] * 6}, res
+
+
+def _rccl_worker(port, q):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from mazero_amd.nets import make_net
+    from mazero_amd.weights import WeightBroadcaster
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    net = make_net(3, 9, seed=3, device=torch.device("cuda", 0))
+    wb = WeightBroadcaster(net, src=0)
+    before = {k: v.clone() for k, v in net.state_dict().items()}
+    wb.publish(4)
+    ok = wb.sync() == 4 and all(torch.equal(before[k], v) for k, v in net.state_dict().items())
+    ok = ok and all(t.is_cuda for t in wb.flat.tensors())
+    q.put(bool(ok))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_broadcast_single_rank():
+    """The RCCL path (backend "nccl" = RCCL on ROCm) on the device model: flat device buffers,
+    index and weights through the collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    ok = q.get(timeout=240)
+    p.join(timeout=60)
+    assert ok
