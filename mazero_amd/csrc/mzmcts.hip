@@ -81,6 +81,11 @@ struct Geo {
     int reg_cap;  // value entries staged in LDS per back-propagation chunk
     // dynamic-LDS byte offsets of k_step
     int oA, oB, oQ, oPP, oVs, oC, oPath, oFlag, oT, oPb, oSq, oLp, oRng, oBoot, oReg, oX, lds;
+    // agent_num > 1 (joint-action trees, general layout only): agents, N*A, and the LDS regions of
+    // the nodes' joint actions [P][N] (bytes), the staged policy / beta / noise [N][A], the
+    // per-agent CDFs [N][A] (double) and the draws [K][N]
+    int N, NA, JP;  // JP: bytes of joint actions per tree (P*N rounded up to 16)
+    int oJ, oJpol, oJbet, oJcp, oJdraw;
 };
 
 struct Dev {
@@ -88,7 +93,8 @@ struct Dev {
     // 32-bit offsets in 256-byte units keeps the kernel arguments small (each pointer would take
     // two SGPRs for the whole kernel).
     char *base;
-    unsigned o_A, o_Bn, o_Q, o_PP, o_C, o_D, o_V, o_R, o_hdr, o_path, o_stats, o_err, o_T, o_pb, o_sq, o_lp, o_seed;
+    unsigned o_J, o_A, o_Bn, o_Q, o_PP, o_C, o_D, o_V, o_R, o_hdr, o_path, o_stats, o_err, o_T, o_pb, o_sq, o_lp, o_seed;
+    __host__ __device__ unsigned char *J() const { return (unsigned char *)(base + (size_t)o_J * 256); }  // [P][N] joint actions (agent_num > 1)
     __host__ __device__ int4 *A() const { return (int4 *)(base + (size_t)o_A * 256); }  // [P] {visit, prior, value, reward}
     __host__ __device__ int4 *Bn() const { return (int4 *)(base + (size_t)o_Bn * 256); }  // [P] {first_child, nc|act<<8|(maxdepth+1)<<16, pred_value, hsx}
     __host__ __device__ float *Q() const { return (float *)(base + (size_t)o_Q * 256); }  // [P] q - parent.pred_value
@@ -311,6 +317,38 @@ __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, co
     return d.R()[(size_t)t * g.W + idx];
 }
 
+// std::discrete_distribution<int>::param_type::_M_initialize (libstdc++ random.tcc:2656-2690) for
+// the distribution whose weight for action `lane` is `bd` (0 for lanes >= A): sequential double
+// sum, p = w / sum, sequential prefix sums, the last forced to 1.0.  Returns this lane's cumulative
+// probability.  Serial chains in blocks of 8 fully unrolled steps (readlane is convergent, so the
+// compiler cannot unroll a runtime-count loop over it by itself).
+__device__ __forceinline__ double cdf_lane(double bd, int A) {
+    const int l = lane_id();
+    double sum = 0.0;
+    int a0 = 0;
+    for (; a0 + 8 <= A; a0 += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += rld(bd, a0 + j);
+    }
+    for (; a0 < A; ++a0) sum += rld(bd, a0);
+    const double p = bd / sum;
+    double acc = rld(p, 0), cp = (l == 0) ? acc : 0.0;
+    a0 = 1;
+    for (; a0 + 8 <= A; a0 += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            acc = acc + rld(p, a0 + j);
+            cp = (l == a0 + j) ? acc : cp;
+        }
+    }
+    for (; a0 < A; ++a0) {
+        acc = acc + rld(p, a0);
+        cp = (l == a0) ? acc : cp;
+    }
+    if (l == A - 1) cp = 1.0;
+    return cp;
+}
+
 // --------------------------------------------------------------------------------------------
 // CTree::expand (cnode.cpp:224-295) for one node, agent_num = 1.  Lane a < A holds the node's
 // policy / beta / noise entry for action a.  Children are created for the distinct sampled actions
@@ -332,32 +370,7 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
     if (A < 2) {
         cnt = (l == 0) ? K : 0;
     } else {
-        // cumulative distribution (param_type::_M_initialize): sequential double sums
-        // (serial chains, in blocks of 8 fully unrolled steps: readlane is convergent, so the
-        // compiler cannot unroll a runtime-count loop over it by itself)
-        const double bd = (l < A) ? (double)bet : 0.0;
-        double sum = 0.0;
-        int a0 = 0;
-        for (; a0 + 8 <= A; a0 += 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sum += rld(bd, a0 + j);
-        }
-        for (; a0 < A; ++a0) sum += rld(bd, a0);
-        const double p = bd / sum;
-        double acc = rld(p, 0), cp = (l == 0) ? acc : 0.0;
-        a0 = 1;
-        for (; a0 + 8 <= A; a0 += 8) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                acc = acc + rld(p, a0 + j);
-                cp = (l == a0 + j) ? acc : cp;
-            }
-        }
-        for (; a0 < A; ++a0) {
-            acc = acc + rld(p, a0);
-            cp = (l == a0) ? acc : cp;
-        }
-        if (l == A - 1) cp = 1.0;
+        const double cp = cdf_lane((l < A) ? (double)bet : 0.0, A);
         if (MZ_STAMPS && stl) {
             asm volatile("" ::"v"(cp));
             e1 = __builtin_amdgcn_s_memtime();
@@ -430,6 +443,114 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
 }
 
 // --------------------------------------------------------------------------------------------
+// CTree::expand (cnode.cpp:224-295) with agent_num = N > 1, K <= 64 (lane k = draw k).  One
+// discrete distribution per agent; draw k takes agent 0..N-1 in turn, two engine words per agent
+// draw (none when A < 2); key = key * 23333 + a_i in 64-bit two's complement (the reference's
+// `long`, which wraps past N = 4); children = the distinct keys in ascending signed order
+// (std::map<long>), beta_hat = count / K, products over agents in agent order.  pol / bet / noi are
+// the node's [N][A] inputs in LDS; cp [N][A] and draw [K][N] are LDS scratch.
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ long long rl64(long long v, int j) {
+    const int lo = __builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffffll), j);
+    const int hi = __builtin_amdgcn_readlane((int)(v >> 32), j);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+__device__ int expand_joint(const Geo &g, const Dev &d, int t, const float *pol, const float *bet, const float *noi,
+                            float eps, int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase,
+                            Lds *s, unsigned char *sJ, double *cp, int *draw, int &err, long long &st_new) {
+    const int l = lane_id();
+    const int N = g.N, A = g.A;
+    if (A >= 2) {
+        for (int i = 0; i < N; ++i) {
+            const double c = cdf_lane((l < A) ? (double)bet[i * A + l] : 0.0, A);
+            if (l < A) cp[i * A + l] = c;
+        }
+        wait_lds();
+    }
+    unsigned long long key = 0;
+    if (l < K) {
+        for (int i = 0; i < N; ++i) {
+            int act = 0;
+            if (A >= 2) {
+                const int w = cursor + 2 * (l * N + i);
+                const double w1 = (double)rng_word_lane(g, d, win, wbase, t, w, err);
+                const double w2 = (double)rng_word_lane(g, d, win, wbase, t, w + 1, err);
+                double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
+                if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+                for (int a = 0; a < A; ++a) act += (cp[i * A + a] < u) ? 1 : 0;  // lower_bound
+            }
+            draw[l * N + i] = act;
+            key = key * 23333ull + (unsigned long long)act;
+        }
+    }
+    if (A >= 2) cursor += 2 * K * N;
+    wait_lds();
+    // distinct keys: first occurrence, multiplicity, rank among the distinct keys (signed order)
+    const long long sk = (long long)key;
+    bool first = l < K;
+    int count = 0;
+    for (int j = 0; j < K; ++j) {
+        const long long kj = rl64(sk, j);
+        if (l < K && kj == sk) {
+            ++count;
+            if (j < l) first = false;
+        }
+    }
+    const unsigned long long fm = ballot(first);
+    int rank = 0;
+    for (unsigned long long m = fm; m; m &= m - 1ull) {
+        const long long kj = rl64(sk, __builtin_ctzll(m));
+        rank += (kj < sk) ? 1 : 0;
+    }
+    const int nc = __popcll(fm);
+    if (tot + nc > g.P) {
+        err |= kErrPool;
+        return 0;
+    }
+    if (first) {
+        const int c = tot + rank;
+        const float bh = (float)count / (float)K;  // betahat_prob = count / sampled_times
+        float beta_prob = 1.0f, pred_prob = 1.0f, prior = 1.0f;
+        for (int i = 0; i < N; ++i) {
+            const int act = draw[l * N + i];
+            const float pa = pol[i * A + act];
+            beta_prob *= bet[i * A + act];
+            pred_prob *= pa;
+            if (eps > 0) {
+                const float p = pa * (1 - eps) + noi[i * A + act] * eps;
+                prior *= p;
+            } else {
+                prior *= pa;
+            }
+        }
+        prior = prior * bh / beta_prob;
+        const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+        const int4 b4 = make_int4(0, pack_y(0, draw[l * N], -1), f2i(0.0f), -1);
+        const size_t gi = (size_t)t * g.P + c;
+        d.A()[gi] = a4;
+        d.Bn()[gi] = b4;
+        d.C()[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d.D()[gi] = make_float4(pred_prob, beta_prob, bh, 0.f);
+        d.Q()[gi] = 0.f;
+        d.PP()[gi] = pv;
+        for (int i = 0; i < N; ++i) {
+            d.J()[(size_t)t * g.JP + (size_t)c * N + i] = (unsigned char)draw[l * N + i];
+            if (sJ) sJ[c * N + i] = (unsigned char)draw[l * N + i];
+        }
+        if (s) {
+            s->A[c] = a4;
+            s->B[c] = b4;
+            s->Q[c] = 0.f;
+            s->PP[c] = pv;
+        }
+    }
+    st_new += nc;
+    tot += nc;
+    return nc;
+}
+
+// --------------------------------------------------------------------------------------------
 // Prepare (CTree_batch::prepare, cnode.cpp:589-614 -> CTree::prepare, cnode.cpp:205-222):
 // generate the tree's mt19937 stream (seed random_seed*2333 + i, cnode.cpp:574) with all four
 // waves, then expand the root with wave 0.
@@ -497,17 +618,35 @@ __global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
     // ---- root expansion by wave 0 ----
     const int l = tid;
     const int A = g.A;
-    const size_t ib = (size_t)t * A;
-    const float pol = (l < A) ? a.policy[ib + l] : 0.f;
-    const float bet = (l < A) ? a.beta[ib + l] : 0.f;
-    const float noi = (l < A) ? a.noise[ib + l] : 0.f;
     const float r = a.reward[t];
     const float v = a.value[t];
     int err = 0;
     int cursor = 0, tot = 1;
     long long st_new = 0;
-    const int nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false,
-                               0u, 0u, nullptr);
+    int nc;
+    if (g.N > 1) {  // joint actions: the root's [N][A] inputs staged in (dynamic) LDS
+        extern __shared__ __attribute__((aligned(16))) unsigned char jsm[];
+        const int NA = g.NA;
+        float *jp = (float *)jsm, *jb = jp + NA, *jn = jb + NA;
+        double *jcp = (double *)(jsm + ((12 * NA + 15) & ~15));
+        int *jd = (int *)(jcp + NA);
+        const size_t ib = (size_t)t * NA;
+        for (int i = l; i < NA; i += kWave) {
+            jp[i] = a.policy[ib + i];
+            jb[i] = a.beta[ib + i];
+            jn[i] = a.noise[ib + i];
+        }
+        wait_lds();
+        nc = expand_joint(g, d, t, jp, jb, jn, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, nullptr, jcp, jd, err,
+                          st_new);
+    } else {
+        const size_t ib = (size_t)t * A;
+        const float pol = (l < A) ? a.policy[ib + l] : 0.f;
+        const float bet = (l < A) ? a.beta[ib + l] : 0.f;
+        const float noi = (l < A) ? a.noise[ib + l] : 0.f;
+        nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false, 0u,
+                         0u, nullptr);
+    }
     if (l == 0) {
         // root: CNode(1,1,1,1,true) (cnode.cpp:217), expanded, visit += 1, subtree.update(value, 0)
         const size_t gi = (size_t)t * g.P;
@@ -1002,7 +1141,7 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // records, q / parent values, RNG window -- issued before one wait; (3) path-node scalars and the
 // value entries the back-propagation needs, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
-template <bool EB, bool SEL, int NC>
+template <bool EB, bool SEL, int NC, bool JOINT>
 __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds s = make_lds<NC>(smem, g);
@@ -1020,7 +1159,10 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     // ---- round 1: everything that does not depend on the tree header, issued with it --------
     float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
     unsigned w1r = 0u, w2r = 0u;
-    const bool have_w = 2 * a.K <= kNxt;
+    const bool have_w = !JOINT && 2 * a.K <= kNxt;
+    float *sJpol = JOINT ? (float *)(smem + g.oJpol) : nullptr;
+    float *sJbet = JOINT ? (float *)(smem + g.oJbet) : nullptr;
+    unsigned char *sJ = JOINT ? (smem + g.oJ) : nullptr;
     if (EB) r_in = a.reward[t];
     if (EB) v_in = a.value[t];
     // gathered row chunks (four named registers: an array here ends up in scratch memory).  A K = 1
@@ -1055,7 +1197,14 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
 #ifdef MZ_PROBE
         pr1 = __builtin_amdgcn_s_memtime();
 #endif
-        if (EB) {
+        if (EB && JOINT) {
+            const size_t ib = (size_t)t * g.NA;
+            for (int i0 = 0; i0 < g.NA; i0 += kWave)
+                if (i0 + l < g.NA) {
+                    glds4(a.policy + ib + i0 + l, sJpol + i0);
+                    glds4(a.beta + ib + i0 + l, sJbet + i0);
+                }
+        } else if (EB) {
             const size_t ib = (size_t)t * g.A;
             if (l < g.A) {
                 pol = a.policy[ib + l];
@@ -1114,11 +1263,14 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
     }
     stamp(ts, 1);
     if (h.err) {  // a dead tree stays dead (both waves see the same header)
-        if (SEL && wv == 0 && l == 0) {
-            a.idx_x[t] = 0;
-            a.idy[t] = t;
-            a.act[t] = 0;
+        if (SEL && wv == 0) {
+            if (l == 0) {
+                a.idx_x[t] = 0;
+                a.idy[t] = t;
+            }
+            if (l < (JOINT ? g.N : 1)) a.act[(size_t)t * (JOINT ? g.N : 1) + l] = 0;
         }
+        wait_vm();
         return;
     }
     int err = 0;
@@ -1155,10 +1307,18 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
             if (wbase + i0 + l < g.W) glds4(d.R() + (size_t)t * g.W + wbase + i0 + l, s.rng + i0);
         if (EB) leaf_b = d.Bn()[nb + h.leaf];  // used after the expansion: no wait here
         if (!EB || !have_w) wait_vm();  // the expansion reads its words from the window
-    } else if (EB) {
-        for (int i0 = 0; i0 <= h.D; i0 += kWave)
-            if (i0 + l <= h.D) glds16(d.C() + nb + s.path[i0 + l].x, s.C + i0);
-        cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
+    } else {
+        if (JOINT) {  // the nodes' joint actions (tree block of JP bytes, 16-byte aligned)
+            const int dw = (tot * g.N + 3) >> 2;
+            const unsigned *src = (const unsigned *)(d.J() + (size_t)t * g.JP);
+            for (int i0 = 0; i0 < dw; i0 += kWave)
+                if (i0 + l < dw) glds4(src + i0 + l, (unsigned *)sJ + i0);
+        }
+        if (EB) {
+            for (int i0 = 0; i0 <= h.D; i0 += kWave)
+                if (i0 + l <= h.D) glds16(d.C() + nb + s.path[i0 + l].x, s.C + i0);
+            cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
+        }
     }
     stamp(ts, 3);
 
@@ -1169,8 +1329,13 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
             // ---- CTree::expand (cnode.cpp:224-295) of the leaf (expand_and_backprop, :452-469) ----
             const int leaf = h.leaf;
             long long st_new = 0;
-            const int nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err,
-                                       st_new, have_w, w1r, w2r, stl);
+            int nc;
+            if (JOINT)
+                nc = expand_joint(g, d, t, sJpol, sJbet, nullptr, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, sJ,
+                                  (double *)(smem + g.oJcp), (int *)(smem + g.oJdraw), err, st_new);
+            else
+                nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new,
+                                 have_w, w1r, w2r, stl);
             stl[MZ_S_EXPANDS] += 1;
             stl[MZ_S_NEW_CHILDREN] += st_new;
             if (!err && l == 0) {
@@ -1210,6 +1375,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
                 xi[3] = err;
             }
         }
+        if (JOINT && wv == 1) wait_vm();  // the joint actions staged for the selection
         __syncthreads();
         if (wv == 1) {
             wait_vm();  // nothing of wave 1 may be in flight when the block ends
@@ -1232,6 +1398,7 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
             h.tot = ntot;
         }
     } else {
+        if (wv == 1) wait_vm();
         __syncthreads();  // wave 1 staged the node records the selection reads
         if (wv == 1) return;
     }
@@ -1249,6 +1416,11 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;
+        }
+        if (JOINT) {
+            wait_lds();
+            if (l < g.N) a.act[(size_t)t * g.N + l] = err ? 0 : (int)sJ[h.leaf * g.N + l];
+        } else if (l == 0) {
             a.act[t] = act;
         }
         stamp(ts, 7);
@@ -1278,10 +1450,12 @@ __global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
                     *(int *)(dst + o2) = *(const int *)(src + o2);
             }
         }
-    } else if (SEL && l == 0) {
-        a.idx_x[t] = 0;
-        a.idy[t] = t;
-        a.act[t] = 0;
+    } else if (SEL) {
+        if (l == 0) {
+            a.idx_x[t] = 0;
+            a.idy[t] = t;
+        }
+        if (l < (JOINT ? g.N : 1)) a.act[(size_t)t * (JOINT ? g.N : 1) + l] = 0;
     }
     stamp(ts, 8);
     // header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
@@ -1357,15 +1531,17 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
     const int t = blockIdx.x;
     const int l = threadIdx.x;
     const int B = g.B, A = g.A;
+    (void)A;
     const size_t nb = (size_t)t * g.P;
     const int4 ra = d.A()[nb];
     const int4 rbn = d.Bn()[nb];
     const int nc = nc_of(uni(rbn.y));
     const int fc = uni(rbn.x);
     float *fout = (float *)out;
+    const int N = g.N, NA = g.NA;
     if (l == 0) {
         fout[t] = (nc > 0) ? i2f(ra.z) : 0.f;
-        out[B + 2 * B * A + t] = nc;
+        out[B + 2 * B * NA + t] = nc;
     }
     const bool has = l < nc;
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
@@ -1376,28 +1552,35 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
         cd = d.D()[nb + fc + l];
     }
     const int act = act_of(cb.y);
-    // marginal visit counts / priors: lane a collects the child whose action is a
-    int mv = 0;
-    float mp = 0.f;
-    for (int j = 0; j < nc; ++j) {
-        const int aj = rl(act, j), vj = rl(ca.x, j);
-        const float pj = rlf(i2f(ca.y), j);
-        if (aj == l) {
-            mv += vj;
-            mp += pj;
+    const unsigned char *jt = d.J() + (size_t)t * g.JP + (size_t)fc * N;  // joint actions (N > 1)
+    // marginal visit counts / priors (cnode.cpp:69-91): cell (agent j, action a) collects, in child
+    // order, every child whose action for agent j is a
+    for (int cell = l; cell < NA; cell += kWave) {
+        const int j = cell / A, av = cell - j * A;
+        int mv = 0;
+        float mp = 0.f;
+        for (int c = 0; c < nc; ++c) {
+            const int aj = (N == 1) ? rl(act, c) : (int)jt[c * N + j];
+            const int vj = rl(ca.x, c);
+            const float pj = rlf(i2f(ca.y), c);
+            if (aj == av) {
+                mv += vj;
+                mp += pj;
+            }
         }
-    }
-    if (l < A) {
-        out[B + (size_t)t * A + l] = mv;
-        fout[B + B * A + (size_t)t * A + l] = mp;
+        out[B + (size_t)t * NA + cell] = mv;
+        fout[B + (size_t)B * NA + (size_t)t * NA + cell] = mp;
     }
     if (l < Wd) {
-        const size_t base = (size_t)2 * B + 2 * (size_t)B * A;
+        const size_t base = (size_t)2 * B + 2 * (size_t)B * NA;
         const size_t o = (size_t)t * Wd + l;
-        const size_t fs = (size_t)B * Wd;
+        const size_t fs = (size_t)B * Wd * N;
         const float val = i2f(ca.z);  // CNode::value(): 0 when not expanded (stored that way)
         const float rew = i2f(ca.w);
-        out[base + MZ_F_ACTIONS * fs + o] = has ? act : 0;
+        if (N == 1)
+            out[base + MZ_F_ACTIONS * fs + o] = has ? act : 0;
+        else
+            for (int i = 0; i < N; ++i) out[base + MZ_F_ACTIONS * fs + o * N + i] = has ? (int)jt[l * N + i] : 0;
         out[base + MZ_F_VISIT_COUNT * fs + o] = has ? ca.x : 0;
         fout[base + MZ_F_PRED_PROBS * fs + o] = has ? cd.x : 0.f;
         fout[base + MZ_F_BETA * fs + o] = has ? cd.y : 0.f;
@@ -1418,6 +1601,7 @@ __global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int W
 // ================================================================================================
 struct mz_batch {
     int B, N, A, K, S, P, E, W, PS, Wd;
+    int NA;  // N * A: per-root policy / marginal entries
     int device;
     Geo geo;
     Dev dev;
@@ -1546,22 +1730,25 @@ struct ArenaPlan {
     }
 };
 
-template <int NC>
+template <int NC, bool JOINT = false>
 void launch_nc(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
     const Geo &g = b->geo;
     if (eb && sel)
-        hipLaunchKernelGGL((k_step<true, true, NC>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
     else if (eb)
-        hipLaunchKernelGGL((k_step<true, false, NC>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<true, false, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev,
+                           a);
     else
-        hipLaunchKernelGGL((k_step<false, true, NC>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<false, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev,
+                           a);
 }
 
-template <int NC>
+template <int NC, bool JOINT = false>
 void set_lds_limit(int lds) {
-    (void)hipFuncSetAttribute((const void *)k_step<true, true, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    (void)hipFuncSetAttribute((const void *)k_step<true, false, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    (void)hipFuncSetAttribute((const void *)k_step<false, true, NC>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const auto attr = hipFuncAttributeMaxDynamicSharedMemorySize;
+    (void)hipFuncSetAttribute((const void *)k_step<true, true, NC, JOINT>, attr, lds);
+    (void)hipFuncSetAttribute((const void *)k_step<true, false, NC, JOINT>, attr, lds);
+    (void)hipFuncSetAttribute((const void *)k_step<false, true, NC, JOINT>, attr, lds);
 }
 
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
@@ -1574,7 +1761,9 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         const long long pe = b->expansions + 1;
         a.pe = (int)(pe < g.PS ? pe : g.PS);
     }
-    switch (b->nc) {
+    if (b->N > 1) {
+        launch_nc<0, true>(b, eb, sel, a);
+    } else switch (b->nc) {
         case 64: launch_nc<64>(b, eb, sel, a); break;
         case 128: launch_nc<128>(b, eb, sel, a); break;
         case 256: launch_nc<256>(b, eb, sel, a); break;
@@ -1614,9 +1803,14 @@ int readback(mz_batch *b, float disc) {
     return MZ_OK;
 }
 
+// Packed readback layout (4-byte words): [B] root value | [B*NA] marginal visits | [B*NA] marginal
+// priors | [B] degree | MZ_F_COUNT x [B*Wd*N] per-child fields (actions fill [B][Wd][N], the
+// others the first B*Wd words).
+size_t rb_deg_base(const mz_batch *b) { return (size_t)b->B + 2 * (size_t)b->B * b->NA; }
 size_t rb_field_base(const mz_batch *b, int field) {
-    return (size_t)2 * b->B + 2 * (size_t)b->B * b->A + (size_t)field * b->B * b->Wd;
+    return rb_deg_base(b) + (size_t)b->B + (size_t)field * b->B * b->Wd * b->N;
 }
+size_t rb_field_width(const mz_batch *b, int field) { return (size_t)b->Wd * (field == MZ_F_ACTIONS ? b->N : 1); }
 
 }  // namespace
 
@@ -1631,28 +1825,33 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     if (!out) return fail(MZ_ERR_ARG, "null output handle");
     *out = nullptr;
     if (B < 1 || A < 1 || K < 1 || S < 0) return fail(MZ_ERR_ARG, "bad tree-batch dimensions");
-    if (N != 1)
-        return fail(MZ_ERR_UNSUPPORTED,
-                    "agent_num != 1: the per-agent sequential search of this fork builds 1-agent trees "
-                    "(mcts_sampled.py:53,89); joint-action trees are not implemented on the GPU yet");
+    if (N < 1) return fail(MZ_ERR_ARG, "agent_num must be >= 1");
     if (A > kMaxActions) return fail(MZ_ERR_UNSUPPORTED, "action_space_size > 64");
+    if (N > 1 && (K > kWave || N > kWave || (long long)N * A > 4096))
+        return fail(MZ_ERR_UNSUPPORTED, "joint-action trees (agent_num > 1) need sampled_times <= 64, "
+                                         "agent_num <= 64 and agent_num * action_space_size <= 4096");
     if (S > 65000) return fail(MZ_ERR_UNSUPPORTED, "simulation_num > 65000");
     if (K > 4096) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 4096");
     auto *b = new mz_batch;
     b->B = B;
     b->N = N;
     b->A = A;
+    b->NA = N * A;
     b->K = K;
     b->S = S;
     b->P = K * (S + 2);
     b->E = S + 1;
     b->PS = S + 2;
-    b->Wd = (K < A ? K : A);
+    {  // max root degree: min(K, A^N)
+        long long an = 1;
+        for (int i = 0; i < N && an < K; ++i) an *= A;
+        b->Wd = (int)(K < an ? K : an);
+    }
     if (b->Wd < 1) b->Wd = 1;
-    // RNG words a search can consume: 2K per expansion (S+1 of them, +1 slack) and at most
+    // RNG words a search can consume: 2KN per expansion (S+1 of them, +1 slack) and at most
     // (leaf depth) words per selection, sum_{s<=S} (s+1); rounded up to whole 624-word blocks.
     {
-        const long long need = 2ll * K * (S + 2) + (long long)(S + 1) * (S + 2) / 2 + kRngWin;
+        const long long need = 2ll * K * N * (S + 2) + (long long)(S + 1) * (S + 2) / 2 + kRngWin;
         b->W = (int)(((need + kMtN - 1) / kMtN) * kMtN);
     }
     if (hipGetDevice(&b->device) != hipSuccess) {
@@ -1701,6 +1900,18 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oBoot = o; o += round16(4 * g.PS);
     g.oReg = o; o += round16(8 * g.reg_cap);
     g.oX = o; o += round16(8 * (MZ_S_COUNT + 2));
+    g.N = N;
+    g.NA = N * A;
+    g.JP = (N > 1) ? round16(b->P * N) : 0;
+    if (N > 1) {
+        g.oJ = o; o += round16(b->P * N);
+        g.oJpol = o; o += round16(4 * g.NA);
+        g.oJbet = o; o += round16(4 * g.NA);
+        g.oJcp = o; o += round16(8 * g.NA);
+        g.oJdraw = o; o += round16(4 * kWave * N);
+    } else {
+        g.oJ = g.oJpol = g.oJbet = g.oJcp = g.oJdraw = 0;
+    }
     g.lds = o;
     // compile-time layout class (pb / sq pUCT tables, value-entry chunks of kRegCap)
     b->nc = 0;
@@ -1712,6 +1923,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
 #ifdef MZ_DYNAMIC_LAYOUT
     b->nc = 0;
 #endif
+    if (N > 1) b->nc = 0;  // joint-action trees use the general layout (joint regions from Geo)
     if (b->nc) {
         g.use_table = 0;
         if (g.reg_cap > kRegCap) g.reg_cap = kRegCap;
@@ -1752,9 +1964,10 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         plan.dev<int2>(d.o_path, (size_t)B * b->PS);
         plan.dev<unsigned>(d.o_R, (size_t)B * b->W);
         plan.dev<float4>(d.o_D, nodes);
-        plan.ptr(&b->sel_dev, (size_t)3 * B);
-        plan.ptr(&b->in_dev, (size_t)B * (2 + 3 * A));
-        b->rb_words = (size_t)2 * B + 2 * (size_t)B * A + (size_t)MZ_F_COUNT * B * b->Wd;
+        plan.ptr(&b->sel_dev, (size_t)B * (2 + N));
+        plan.ptr(&b->in_dev, (size_t)B * (2 + 3 * (size_t)N * A));
+        b->rb_words = (size_t)2 * B + 2 * (size_t)B * N * A + (size_t)MZ_F_COUNT * B * b->Wd * N;
+        if (N > 1) plan.dev<unsigned char>(d.o_J, (size_t)B * g.JP);
         plan.ptr(&b->rb_dev, b->rb_words);
         plan.dev<int2>(d.o_V, nodes * b->E);
         rc = plan.allocate(b, d);
@@ -1776,7 +1989,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         return fail(MZ_ERR_DEVICE, "device initialisation failed");
     }
     if (g.lds > 64 * 1024) {
-        switch (b->nc) {
+        if (N > 1) set_lds_limit<0, true>(g.lds);
+        else switch (b->nc) {
             case 64: set_lds_limit<64>(g.lds); break;
             case 128: set_lds_limit<128>(g.lds); break;
             case 256: set_lds_limit<256>(g.lds); break;
@@ -1817,7 +2031,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
     int rc = ensure_device(b);
     if (rc) return rc;
-    const size_t B = b->B, NA = (size_t)b->A;
+    const size_t B = b->B, NA = (size_t)b->NA;
     PrepArgs a;
     if (mem == MZ_MEM_HOST) {
         float *p = b->in_dev;
@@ -1843,7 +2057,8 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     a.eps = noise_eps;
     a.K = K;
     HIP_TRY(hipMemsetAsync(b->dev.err(), 0, sizeof(int), b->stream));
-    hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), 0, b->stream, b->geo, b->dev, a);
+    const size_t jl = (b->N > 1) ? (size_t)((12 * b->NA + 15) & ~15) + 8 * (size_t)b->NA + 4 * (size_t)kWave * b->N : 0;
+    hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), jl, b->stream, b->geo, b->dev, a);
     HIP_TRY(hipGetLastError());
     b->rb_valid = b->rb_dev_valid = false;
     b->prepared = true;
@@ -1876,20 +2091,20 @@ int mz_select(mz_batch *b, float c2, float c1, float discount, int32_t *idx_x, i
     rc = launch_step(b, false, true, a);
     if (rc) return rc;
     if (mem == MZ_MEM_HOST) {
-        std::vector<int32_t> tmp(3 * (size_t)b->B);
+        std::vector<int32_t> tmp((size_t)b->B * (2 + b->N));
         HIP_TRY(hipMemcpyAsync(tmp.data(), b->sel_dev, sizeof(int32_t) * tmp.size(), hipMemcpyDeviceToHost, b->stream));
         rc = check_device_errors(b);
         if (rc) return rc;
         std::memcpy(idx_x, tmp.data(), sizeof(int32_t) * b->B);
         std::memcpy(idy, tmp.data() + b->B, sizeof(int32_t) * b->B);
-        std::memcpy(actions, tmp.data() + 2 * b->B, sizeof(int32_t) * b->B);
+        std::memcpy(actions, tmp.data() + 2 * b->B, sizeof(int32_t) * b->B * b->N);
     }
     return MZ_OK;
 }
 
 static int expand_inputs(mz_batch *b, const float *rewards, const float *values, const float *policy,
                          const float *beta, int mem, StepArgs &a) {
-    const size_t B = b->B, NA = (size_t)b->A;
+    const size_t B = b->B, NA = (size_t)b->NA;
     if (mem == MZ_MEM_HOST) {
         float *p = b->in_dev;
         HIP_TRY(hipMemcpyAsync(p, rewards, 4 * B, hipMemcpyHostToDevice, b->stream));
@@ -2025,7 +2240,7 @@ int mz_get_roots_marginal_visit_count(mz_batch *b, int32_t *out, int mem) {
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
                                 : readback(b, b->rb_valid ? b->rb_disc : 0.f);
     if (rc) return rc;
-    const size_t n = (size_t)b->B * b->A;
+    const size_t n = (size_t)b->B * b->NA;
     if (mem == MZ_MEM_DEVICE) {
         HIP_TRY(hipMemcpyAsync(out, b->rb_dev + b->B, 4 * n, hipMemcpyDeviceToDevice, b->stream));
         return MZ_OK;
@@ -2041,7 +2256,7 @@ int mz_get_roots_marginal_priors(mz_batch *b, float *out, int mem) {
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
                                 : readback(b, b->rb_valid ? b->rb_disc : 0.f);
     if (rc) return rc;
-    const size_t n = (size_t)b->B * b->A;
+    const size_t n = (size_t)b->B * b->NA;
     if (mem == MZ_MEM_DEVICE) {
         HIP_TRY(hipMemcpyAsync(out, b->rb_dev + b->B + n, 4 * n, hipMemcpyDeviceToDevice, b->stream));
         return MZ_OK;
@@ -2057,7 +2272,7 @@ int mz_get_num_children_of_root(mz_batch *b, int tree_id, int32_t *out) {
     if (rc) return rc;
     rc = readback(b, b->rb_valid ? b->rb_disc : 0.f);
     if (rc) return rc;
-    *out = b->rb_host[(size_t)b->B + 2 * (size_t)b->B * b->A + tree_id];
+    *out = b->rb_host[rb_deg_base(b) + tree_id];
     return MZ_OK;
 }
 
@@ -2075,8 +2290,9 @@ int mz_get_root_sampled(mz_batch *b, int field, int tree_id, float discount, voi
     if (rc) return rc;
     rc = readback(b, field == MZ_F_QVALUES ? discount : (b->rb_valid ? b->rb_disc : discount));
     if (rc) return rc;
-    const int deg = b->rb_host[(size_t)b->B + 2 * (size_t)b->B * b->A + tree_id];
-    std::memcpy(out, b->rb_host.data() + rb_field_base(b, field) + (size_t)tree_id * b->Wd, 4 * (size_t)deg);
+    const int deg = b->rb_host[rb_deg_base(b) + tree_id];
+    const size_t per = (field == MZ_F_ACTIONS) ? (size_t)b->N : 1;
+    std::memcpy(out, b->rb_host.data() + rb_field_base(b, field) + (size_t)tree_id * b->Wd * per, 4 * (size_t)deg * per);
     return MZ_OK;
 }
 
@@ -2088,8 +2304,8 @@ int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *ou
     const float disc = field == MZ_F_QVALUES ? discount : ((b->rb_valid || b->rb_dev_valid) ? b->rb_disc : discount);
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, disc) : readback(b, disc);
     if (rc) return rc;
-    const size_t n = (size_t)b->B * b->Wd;
-    const size_t dego = (size_t)b->B + 2 * (size_t)b->B * b->A;
+    const size_t n = (size_t)b->B * rb_field_width(b, field);
+    const size_t dego = rb_deg_base(b);
     if (mem == MZ_MEM_DEVICE) {
         HIP_TRY(hipMemcpyAsync(out, b->rb_dev + rb_field_base(b, field), 4 * n, hipMemcpyDeviceToDevice, b->stream));
         if (degrees)

@@ -281,3 +281,61 @@ def test_graph_of_one_step_replayed(gpu_lib, port_lib):
     a, b = readbacks(tb, g), readbacks(ref, g)
     for k in ("root_values", "marginal_visit_count", "sampled_qvalues"):
         assert np.array_equal(a[k], b[k]), k
+
+
+# ---- agent_num > 1: joint-action trees (upstream MAZero semantics) ----------
+JOINT = [
+    # (name, B, N, A, K, S)
+    ("matrix_n2_k5", 8, 2, 3, 5, 25),
+    ("3m_n3_k5", 32, 3, 9, 5, 30),
+    ("n2_k1_chain", 16, 2, 9, 1, 30),
+    ("n5_k10_keywrap", 16, 5, 11, 10, 20),  # 23333^5 overflows int64: two's-complement key order
+    ("n6_a4_k16", 8, 6, 4, 16, 15),
+    ("n2_a1", 4, 2, 1, 3, 10),               # single-action agents draw no engine words
+]
+
+
+def _joint_run(lib, B, N, A, K, S, seed):
+    from mazero_amd.cytree import Tree_batch
+
+    rng = np.random.default_rng(seed)
+    pol = lambda: rng.dirichlet([1.0] * A, (B, N)).astype(np.float32) if A > 1 else np.ones((B, N, A), np.float32)  # noqa: E731
+    p0, b0 = pol(), pol()
+    noise = rng.dirichlet([0.3] * A, (B, N)).astype(np.float32) if A > 1 else np.ones((B, N, A), np.float32)
+    r0 = (0.1 * rng.standard_normal(B)).astype(np.float32)
+    v0 = rng.standard_normal(B).astype(np.float32)
+    tb = Tree_batch(B, N, A, K, S, 0.01, 17, 0.75, 0.8, lib=lib)
+    tb.prepare(r0, v0, p0, b0, K, 0.25, noise)
+    rec = []
+    for s in range(S):
+        ix, iy, act = tb.batch_selection(19652.0, 1.25, 0.997)
+        rec.append((np.asarray(ix), np.asarray(act).copy()))
+        r = (0.1 * rng.standard_normal(B)).astype(np.float32)
+        v = rng.standard_normal(B).astype(np.float32)
+        p, b = pol(), pol()
+        tb.batch_expansion_and_backup(s + 1, 0.997, K, r, v, p, b)
+    out = dict(values=tb.get_roots_values(), mv=tb.get_roots_marginal_visit_count(),
+               mp=tb.get_roots_marginal_priors(), q=tb.get_roots_sampled_qvalues(0.997),
+               acts=tb.get_roots_sampled_actions(), vc=tb.get_roots_sampled_visit_count(),
+               pr=tb.get_roots_sampled_priors(), bh=tb.get_roots_sampled_beta_hat())
+    return rec, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,B,N,A,K,S", JOINT, ids=[j[0] for j in JOINT])
+def test_joint_action_trees_vs_port(gpu_lib, port_lib, name, B, N, A, K, S):
+    rec_g, out_g = _joint_run(gpu_lib, B, N, A, K, S, 3)
+    rec_c, out_c = _joint_run(port_lib, B, N, A, K, S, 3)
+    for s, ((ig, ag), (ic, ac)) in enumerate(zip(rec_g, rec_c)):
+        np.testing.assert_array_equal(ig, ic, err_msg=f"idx sim {s}")
+        np.testing.assert_array_equal(ag, ac, err_msg=f"actions sim {s}")
+        assert ag.shape == (B, N)
+    for k in ("values", "mv", "mp"):
+        g, c = out_g[k], out_c[k]
+        assert g.shape == c.shape and g.dtype == c.dtype, k
+        np.testing.assert_array_equal(g.view(np.int32), c.view(np.int32), err_msg=k)
+    for k in ("q", "acts", "vc", "pr", "bh"):
+        for i, (g, c) in enumerate(zip(out_g[k], out_c[k])):
+            assert g.shape == c.shape, (k, i)
+            np.testing.assert_array_equal(g.view(np.int32), c.view(np.int32), err_msg=f"{k}[{i}]")
+    assert (out_g["mv"].sum(axis=2) == S).all()  # every agent's marginal sums to the simulations

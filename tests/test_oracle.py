@@ -122,3 +122,19 @@ def test_ptree_joint_action_matches_reference(ref_lib):
 
 
 saved = []
+
+
+def test_port_joint_action_trees_match_reference(ref_lib, port_lib):
+    """agent_num > 1 on the CPU port vs the reference ctree: the checker of the GPU joint-action
+    kernels (tests/test_gpu_parity.py::test_joint_action_trees_vs_port), incl. int64 key wrap."""
+    import test_gpu_parity as T
+
+    for name, B, N, A, K, S in T.JOINT:
+        rr, orf = T._joint_run(ref_lib, B, N, A, K, S, 3)
+        rp, op = T._joint_run(port_lib, B, N, A, K, S, 3)
+        for (ia, aa), (ib, ab) in zip(rr, rp):
+            assert np.array_equal(ia, ib) and np.array_equal(aa, ab), name
+        for k in ("values", "mv", "mp"):
+            assert np.array_equal(orf[k].view(np.int32), op[k].view(np.int32)), (name, k)
+        for k in ("q", "acts", "vc", "pr", "bh"):
+            assert all(np.array_equal(g.view(np.int32), c.view(np.int32)) for g, c in zip(orf[k], op[k])), (name, k)
