@@ -27,6 +27,7 @@ Model interface (core/model.py:45-79): `prediction(h) -> (policy_logits [B,N,A],
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from typing import List, NamedTuple, Tuple
 
 import numpy as np
@@ -104,8 +105,9 @@ class _SearchLoop:
     Every input is copied into the static buffers before a run, and the tree seed lives in device
     memory (mz_reseed), so replaying the graph is a new search."""
 
-    def __init__(self, tb, B, A, N, cur, hidden, dev):
+    def __init__(self, tb, B, A, N, cur, hidden, dev, model):
         self.tb, self.B, self.A, self.N, self.cur, self.dev = tb, B, A, N, cur, dev
+        self.model_ref = weakref.ref(model)  # the captured graph reads this model's parameters
         self.root = torch.empty_like(hidden.reshape(B, -1))
         self.rin = [torch.empty(n, dtype=torch.float32, device=dev) for n in (B, B, B * A, B * A, B * A)]
         self.sel = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev),
@@ -279,8 +281,8 @@ class SampledMCTS:
             tb = self._tree(B, seed, dev)
             key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), tuple(hidden.shape), hidden.dtype)
             st = _LOOPS.get(key)
-            if st is None:
-                st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev)
+            if st is None or st.model_ref() is not model:  # ids are reused once an object is freed
+                st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model)
             st.load(hidden, (rr, rv, rp, rb, rn), factor)
             with torch.no_grad():
                 if not self.use_graph or st.runs == 0:
