@@ -280,6 +280,8 @@ class SampledMCTS:
         with torch.cuda.device(dev):
             tb = self._tree(B, seed, dev)
             key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), tuple(hidden.shape), hidden.dtype)
+            for k in [k for k, v in _LOOPS.items() if v.model_ref() is None]:
+                del _LOOPS[k]  # loops (graph, pool) of models that no longer exist
             st = _LOOPS.get(key)
             if st is None or st.model_ref() is not model:  # ids are reused once an object is freed
                 st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model)
