@@ -132,6 +132,15 @@ struct PrepArgs {
     int K;
 };
 
+// Per-handle constants, written once to device memory at mz_create: kernels take a pointer to
+// them, so the kernel-argument block is only that pointer plus the launch's own arguments (~120 B).
+// Large by-value kernel arguments are expensive in HIP graphs, whose kernel nodes keep a copy of
+// every launch's argument block.
+struct Params {
+    Geo g;
+    Dev d;
+};
+
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -567,7 +576,9 @@ __device__ __forceinline__ unsigned mt_temper(unsigned z) {
     return z;
 }
 
-__global__ __launch_bounds__(256) void k_prepare(Geo g, Dev d, PrepArgs a) {
+__global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm, PrepArgs a) {
+    const Geo g = prm->g;
+    const Dev d = prm->d;
     __shared__ unsigned mt[kMtN];
     __shared__ unsigned w0[kMtN];
     const int t = blockIdx.x;
@@ -1142,7 +1153,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // value entries the back-propagation needs, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
 template <bool EB, bool SEL, int NC, bool JOINT>
-__global__ __launch_bounds__(128) void k_step(Geo g, Dev d, StepArgs a) {
+__global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, StepArgs a) {
+    const Geo g = prm->g;
+    const Dev d = prm->d;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds s = make_lds<NC>(smem, g);
     const int t = blockIdx.x;
@@ -1527,7 +1540,9 @@ __global__ __launch_bounds__(64) void k_gather(const char *pool, long long strid
 //   [B] root value | [B*A] marginal visits | [B*A] marginal priors | [B] degree |
 //   MZ_F_COUNT x [B*Wd] per-child fields padded with zeros to Wd = max degree
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_readback(Geo g, Dev d, float disc, int Wd, int *out) {
+__global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm, float disc, int Wd, int *out) {
+    const Geo g = prm->g;
+    const Dev d = prm->d;
     const int t = blockIdx.x;
     const int l = threadIdx.x;
     const int B = g.B, A = g.A;
@@ -1619,6 +1634,7 @@ struct mz_batch {
     bool prepared = false;
     long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
     int nc = 0;                // k_step layout class (0 = layout from Geo)
+    Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
 };
 
 namespace {
@@ -1734,13 +1750,11 @@ template <int NC, bool JOINT = false>
 void launch_nc(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
     const Geo &g = b->geo;
     if (eb && sel)
-        hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev, a);
+        hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, b->prm, a);
     else if (eb)
-        hipLaunchKernelGGL((k_step<true, false, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev,
-                           a);
+        hipLaunchKernelGGL((k_step<true, false, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, b->prm, a);
     else
-        hipLaunchKernelGGL((k_step<false, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, g, b->dev,
-                           a);
+        hipLaunchKernelGGL((k_step<false, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, b->prm, a);
 }
 
 template <int NC, bool JOINT = false>
@@ -1761,9 +1775,12 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         const long long pe = b->expansions + 1;
         a.pe = (int)(pe < g.PS ? pe : g.PS);
     }
+#ifndef MZ_NO_JOINT
     if (b->N > 1) {
         launch_nc<0, true>(b, eb, sel, a);
-    } else switch (b->nc) {
+    } else
+#endif
+    switch (b->nc) {
         case 64: launch_nc<64>(b, eb, sel, a); break;
         case 128: launch_nc<128>(b, eb, sel, a); break;
         case 256: launch_nc<256>(b, eb, sel, a); break;
@@ -1782,7 +1799,7 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
 // Packed readback computed on the device (stream-ordered, no synchronisation).
 int readback_dev(mz_batch *b, float disc) {
     if (b->rb_dev_valid && b->rb_disc == disc) return MZ_OK;
-    hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->geo, b->dev, disc, b->Wd, b->rb_dev);
+    hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, disc, b->Wd, b->rb_dev);
     HIP_TRY(hipGetLastError());
     b->rb_dev_valid = true;
     b->rb_valid = false;
@@ -1948,6 +1965,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     // into as few 2 MiB pages as possible.
     {
         ArenaPlan plan;
+        plan.ptr(&b->prm, 1);
         plan.dev<TreeHdr>(d.o_hdr, (size_t)B);
         plan.dev<long long>(d.o_stats, (size_t)B * MZ_S_COUNT);
         plan.dev<int>(d.o_err, 1);
@@ -1977,11 +1995,13 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         mz_destroy(b);
         return fail(MZ_ERR_DEVICE, m);
     }
+    const Params host_params{b->geo, b->dev};
     std::vector<float> lp(b->PS + 1 + kWave, 0.f);
     lp[0] = 1.0f;
     for (int k = 1; k < b->PS + 1; ++k) lp[k] = lp[k - 1] * lam;  // lam_pow chain (utils.cpp:25-27)
     if (hipMemcpy(d.lp(), lp.data(), sizeof(float) * lp.size(), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(d.seed(), &seed, sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(b->prm, &host_params, sizeof(Params), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(d.hdr(), 0, sizeof(TreeHdr) * B) != hipSuccess ||
         hipMemset(d.stats(), 0, sizeof(long long) * B * MZ_S_COUNT) != hipSuccess ||
         hipMemset(d.err(), 0, sizeof(int)) != hipSuccess) {
@@ -1989,8 +2009,11 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         return fail(MZ_ERR_DEVICE, "device initialisation failed");
     }
     if (g.lds > 64 * 1024) {
+#ifndef MZ_NO_JOINT
         if (N > 1) set_lds_limit<0, true>(g.lds);
-        else switch (b->nc) {
+        else
+#endif
+        switch (b->nc) {
             case 64: set_lds_limit<64>(g.lds); break;
             case 128: set_lds_limit<128>(g.lds); break;
             case 256: set_lds_limit<256>(g.lds); break;
@@ -2058,7 +2081,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     a.K = K;
     HIP_TRY(hipMemsetAsync(b->dev.err(), 0, sizeof(int), b->stream));
     const size_t jl = (b->N > 1) ? (size_t)((12 * b->NA + 15) & ~15) + 8 * (size_t)b->NA + 4 * (size_t)kWave * b->N : 0;
-    hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), jl, b->stream, b->geo, b->dev, a);
+    hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), jl, b->stream, b->prm, a);
     HIP_TRY(hipGetLastError());
     b->rb_valid = b->rb_dev_valid = false;
     b->prepared = true;

@@ -40,3 +40,13 @@ print("replay seed7 == eager seed7:", np.array_equal(g1[0], e1[0]), np.array_equ
 tb.reseed(9); g.replay(); tb.state_changed(); g9 = vals()
 print("replay seed9 == eager seed9:", np.array_equal(g9[0], e9[0]), np.array_equal(g9[1], e9[1]))
 print("seed7 != seed9:", not np.array_equal(e1[1], e9[1]))
+
+ok = True
+for rep in range(8):
+    sd = 100 + rep
+    tb.reseed(sd); search(); ev = vals()
+    tb.reseed(sd); g.replay(); tb.state_changed(); gv = vals()
+    same = np.array_equal(ev[0], gv[0]) and np.array_equal(ev[1], gv[1])
+    ok &= same
+    print("rep", rep, "replay == eager:", same, flush=True)
+print("ALL OK" if ok else "MISMATCH")
