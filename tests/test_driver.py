@@ -314,7 +314,7 @@ def test_driver_graph_replay_matches_oracle(K, port_lib):
     rs_o, rs_d = np.random.RandomState(5), np.random.RandomState(5)
     oracle = OracleSampledMCTS(cfg, rs_o, port_lib)
     drv = SampledMCTS(cfg, rs_d, use_graph=True)
-    for step in range(4):
+    for step in range(6):  # eager, capture + replay, then four pure replays
         out, legal = make_root_batch(net, B, 64, seed=100 + step, device=dev, legal_zero_frac=0.25)
         factor = np.random.default_rng(step).integers(0, A, size=(B, cur)).astype(np.int32)
         exp = oracle.batch_search(net, out, cur, factor, N, legal, device=dev, add_noise=True)
