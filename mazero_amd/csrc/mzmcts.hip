@@ -757,29 +757,31 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
     const int l = lane_id();
     const unsigned long long b0 = (MZ_STAMPS != 0) ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long b1 = 0, bw = 0;
-    // bootstrap values (cnode.cpp:424,448)
+    // bootstrap values (cnode.cpp:424,448): b_{i-1} = reward_i + discount * b_i from b_D = value,
+    // one f32 multiply and one add per level, in the reference's order.  Lane j holds level
+    // lo + j of a chunk of up to 64 levels; every step shifts the chunk down one lane with DPP
+    // (wave_shl:1: lane j receives lane j+1) and recomputes all lanes at once, so after
+    // (hi - lo) steps lane j holds exactly the sequential recurrence's b (each lane's last update
+    // uses its converged upper neighbour).  No cross-lane round trip per level.
     {
-        float b = value;
-        if (l == 0) s.boot[D] = b;
-        for (int base = D; base >= 1; base -= kWave) {
-            const int i = base - l;
-            // the leaf's reward is this simulation's input (the expansion wave stores it)
-            const float r = (i >= 1) ? ((i == D) ? reward : i2f(s.A[s.path[i].x].w)) : 0.f;
-            const int n = base < kWave ? base : kWave;
-            float mine = 0.f;
-            int k = 0;
-            for (; k + 8 <= n; k += 8) {  // blocks of 8 fully unrolled steps (see expand_node)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    b = rlf(r, k + j) + disc * b;
-                    mine = (l == k + j) ? b : mine;
-                }
+        float carry = value;
+        int hi = D;
+        while (true) {
+            const int lo = hi > 63 ? hi - 63 : 0;
+            const int nl = hi - lo;  // steps of this chunk
+            const int lev = lo + l;
+            float rn = 0.f;  // reward of the level above this lane's
+            if (lev < hi) rn = (lev + 1 == D) ? reward : i2f(s.A[s.path[lev + 1].x].w);
+            float b = (l == nl) ? carry : 0.f;
+            for (int k = 0; k < nl; ++k) {
+                const float up = i2f(__builtin_amdgcn_update_dpp(f2i(b), f2i(b), 0x130, 0xf, 0xf, false));
+                const float nb = rn + disc * up;
+                b = (l < nl) ? nb : b;
             }
-            for (; k < n; ++k) {
-                b = rlf(r, k) + disc * b;
-                mine = (l == k) ? b : mine;
-            }
-            if (l < n) s.boot[base - l - 1] = mine;
+            if (l <= nl) s.boot[lev] = b;
+            if (lo == 0) break;
+            carry = rlf(b, 0);
+            hi = lo;
         }
     }
     if (MZ_STAMPS) {

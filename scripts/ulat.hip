@@ -72,6 +72,14 @@ __global__ void k_dma(const int4 *src, int n16, unsigned long long *out) {
 
 __global__ void k_empty() {}
 
+// DPP wave shifts: out[l] = value lane l receives from (lane index + 100) under each control
+__global__ void k_dpp(int *out) {
+    const int l = threadIdx.x;
+    const int v = l + 100;
+    out[l] = __builtin_amdgcn_update_dpp(-1, v, 0x130, 0xf, 0xf, false);        // wave_shl:1
+    out[64 + l] = __builtin_amdgcn_update_dpp(-1, v, 0x138, 0xf, 0xf, false);   // wave_shr:1
+}
+
 // instruction-fetch cost: 2048 straight-line VALU ops vs the same count in a 16-op loop
 __global__ void k_straight(unsigned long long *out) {
     unsigned long long t0 = memtime();
@@ -170,6 +178,15 @@ int main() {
         hipLaunchKernelGGL(k_looped, dim3(B), dim3(64), 0, 0, out);
         CK(hipMemcpy(h.data(), out, B * 8, hipMemcpyDeviceToHost));
         printf("2048 VALU ops: straight-line %.0f cycles, looped %.0f cycles\n", a, med(B));
+    }
+    {
+        int *dd;
+        CK(hipMalloc(&dd, 128 * 4));
+        hipLaunchKernelGGL(k_dpp, dim3(1), dim3(64), 0, 0, dd);
+        std::vector<int> hv(128);
+        CK(hipMemcpy(hv.data(), dd, 128 * 4, hipMemcpyDeviceToHost));
+        printf("dpp wave_shl:1 lanes 0,1,15,16,62,63 get: %d %d %d %d %d %d\n", hv[0], hv[1], hv[15], hv[16], hv[62], hv[63]);
+        printf("dpp wave_shr:1 lanes 0,1,15,16,62,63 get: %d %d %d %d %d %d\n", hv[64], hv[65], hv[79], hv[80], hv[126], hv[127]);
     }
     hipStream_t st;
     CK(hipStreamCreate(&st));
