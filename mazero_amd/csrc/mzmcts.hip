@@ -265,7 +265,7 @@ struct Layout {
     static constexpr int oBoot = oRng + r16(4 * kRngWin);
     static constexpr int oReg = oBoot + r16(4 * NC);
     static constexpr int oX = oReg + r16(8 * kRegCap);
-    static constexpr int total = oX + r16(8 * (MZ_S_COUNT + 2));
+    static constexpr int total = oX + r16(8 * (2 * MZ_S_COUNT + 2));
 };
 
 template <int NC>
@@ -1247,7 +1247,9 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
         }
     }
     long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
-    const long long st_old = (wv == 0 && l < MZ_S_COUNT) ? st[l] : 0;
+    // counters written per launch: the algorithmic ones, plus the cycle stamps in diagnostic builds
+    constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
+    const long long st_old = (wv == 0 && l < kStatN) ? st[l] : 0;
     TreeHdr h;
     {
         const TreeHdr *hp = d.hdr() + t;
@@ -1374,16 +1376,11 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
                 stl[MZ_S_CYC_W1_BACKUP] += (long long)(ts[5] - ts[4]);
                 stl[MZ_S_CYC_W1_SYNC] += (long long)(ts[5] - ts[0]);  // wave 1's whole span
             }
-            if (l < MZ_S_COUNT) {
-                long long mine = 0;
-#pragma unroll
-                for (int k = 0; k < MZ_S_COUNT; ++k)
-                    if (l == k) mine = stl[k];
-                xst[l] = mine;
-            }
             if (l == 0) {
-                float *xf = (float *)(xst + MZ_S_COUNT);
-                int *xi = (int *)(xst + MZ_S_COUNT);
+#pragma unroll
+                for (int k = 0; k < kStatN; ++k) xst[MZ_S_COUNT + k] = stl[k];  // wave 1's counters
+                float *xf = (float *)(xst + 2 * MZ_S_COUNT);
+                int *xi = (int *)(xst + 2 * MZ_S_COUNT);
                 xf[0] = h.mm_min;
                 xf[1] = h.mm_max;
                 xi[2] = h.mm_cnt;
@@ -1398,15 +1395,12 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
         }
         // wave 0: merge wave 1's results
         {
-            const float *xf = (const float *)(xst + MZ_S_COUNT);
-            const int *xi = (const int *)(xst + MZ_S_COUNT);
+            const float *xf = (const float *)(xst + 2 * MZ_S_COUNT);
+            const int *xi = (const int *)(xst + 2 * MZ_S_COUNT);
             h.mm_min = unif(xf[0]);
             h.mm_max = unif(xf[1]);
             h.mm_cnt = uni(xi[2]);
             err |= uni(xi[3]);
-            const long long o = (l < MZ_S_COUNT) ? xst[l] : 0;
-#pragma unroll
-            for (int k = 0; k < MZ_S_COUNT; ++k) stl[k] += (k == l) ? o : 0;  // lane k owns counter k
         }
         if (!err) {
             h.cursor = cursor;
@@ -1511,12 +1505,14 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
         for (int k = 0; k < 9; ++k) stl[MZ_S_CYC_HEADER + k] += (long long)(ts[k + 1] - ts[k]);
         stl[MZ_S_STAMPED] += 1;
     }
-    // per-tree statistics: lane k owns counter k
-    long long mine = 0;
+    // per-tree statistics: wave 0's counters through LDS (lane 0 writes, lane k reads counter k),
+    // plus wave 1's when it back-propagated
+    if (l == 0) {
 #pragma unroll
-    for (int k = 0; k < MZ_S_COUNT; ++k)
-        if (l == k) mine = stl[k];
-    if (l < MZ_S_COUNT) st[l] = st_old + mine;
+        for (int k = 0; k < kStatN; ++k) xst[k] = stl[k];
+    }
+    wait_lds();
+    if (l < kStatN) st[l] = st_old + xst[l] + (EB ? xst[MZ_S_COUNT + l] : 0ll);
     if (l == 0 && err) atomicOr(d.err(), err);
 }
 
@@ -1918,7 +1914,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oRng = o; o += round16(4 * kRngWin);
     g.oBoot = o; o += round16(4 * g.PS);
     g.oReg = o; o += round16(8 * g.reg_cap);
-    g.oX = o; o += round16(8 * (MZ_S_COUNT + 2));
+    g.oX = o; o += round16(8 * (2 * MZ_S_COUNT + 2));
     g.N = N;
     g.NA = N * A;
     g.JP = (N > 1) ? round16(b->P * N) : 0;
