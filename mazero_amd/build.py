@@ -35,6 +35,9 @@ FLAGS = [
     "-fno-fast-math",
     "-Wall",
     "-Wno-unused-function",
+    # the first 16 dwords of scalar kernel arguments arrive in SGPRs at wave launch
+    "-mllvm",
+    "-amdgpu-kernarg-preload-count=16",
 ]
 
 

@@ -825,7 +825,7 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
                 }
                 ent_r += nv;
             }
-            const float4 cw = s.C[i];
+            const float4 cw = s.C[n];  // staged per node in round 1
             float ws = cw.x, tw = cw.y;
             const float lp = s.lp[dep];
             const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
@@ -1154,10 +1154,33 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // records, q / parent values, RNG window -- issued before one wait; (3) path-node scalars and the
 // value entries the back-propagation needs, in flight while the leaf is expanded.
 // --------------------------------------------------------------------------------------------
+// Scalar arguments, the ones each wave needs first leading: with kernel-argument preloading
+// (-mllvm -amdgpu-kernarg-preload-count) the first 16 dwords arrive in SGPRs at wave launch, so the
+// round-1 addresses do not wait for a kernel-argument load.
 template <bool EB, bool SEL, int NC, bool JOINT>
-__global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, StepArgs a) {
+__global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, const float *reward, const float *value,
+                                              const float *policy, const float *beta, int hsx, int ne, int pe, int K,
+                                              float discount, const char *pool, long long pool_stride,
+                                              long long row_bytes, char *gather_out, int *idx_x, int *idy, int *act) {
     const Geo g = prm->g;
     const Dev d = prm->d;
+    StepArgs a;
+    a.reward = reward;
+    a.value = value;
+    a.policy = policy;
+    a.beta = beta;
+    a.hsx = hsx;
+    a.ne = ne;
+    a.pe = pe;
+    a.K = K;
+    a.discount = discount;
+    a.pool = pool;
+    a.pool_stride = pool_stride;
+    a.row_bytes = row_bytes;
+    a.gather_out = gather_out;
+    a.idx_x = idx_x;
+    a.idy = idy;
+    a.act = act;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     Lds s = make_lds<NC>(smem, g);
     const int t = blockIdx.x;
@@ -1236,7 +1259,10 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
                 glds16(d.A() + nb + i0 + l, s.A + i0);
                 glds16(d.Bn() + nb + i0 + l, s.B + i0);
                 glds4(d.PP() + nb + i0 + l, s.PP + i0);
-                if (EB) glds4(d.Q() + nb + i0 + l, s.Q + i0);
+                if (EB) {
+                    glds4(d.Q() + nb + i0 + l, s.Q + i0);
+                    glds16(d.C() + nb + i0 + l, s.C + i0);  // value-set scalars, read by node
+                }
             }
         }
         if (EB) {
@@ -1303,7 +1329,10 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
                 glds16(d.A() + nb + i0 + l, s.A + i0);
                 glds16(d.Bn() + nb + i0 + l, s.B + i0);
                 glds4(d.PP() + nb + i0 + l, s.PP + i0);
-                if (EB) glds4(d.Q() + nb + i0 + l, s.Q + i0);
+                if (EB) {
+                    glds4(d.Q() + nb + i0 + l, s.Q + i0);
+                    glds16(d.C() + nb + i0 + l, s.C + i0);
+                }
             }
         }
         if (EB)
@@ -1332,8 +1361,6 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, St
                 if (i0 + l < dw) glds4(src + i0 + l, (unsigned *)sJ + i0);
         }
         if (EB) {
-            for (int i0 = 0; i0 <= h.D; i0 += kWave)
-                if (i0 + l <= h.D) glds16(d.C() + nb + s.path[i0 + l].x, s.C + i0);
             cnt0 = stage_regions(g, d, s, t, h.D, 0, n0, nv0, need0, off0);
         }
     }
@@ -1747,12 +1774,18 @@ struct ArenaPlan {
 template <int NC, bool JOINT = false>
 void launch_nc(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
     const Geo &g = b->geo;
+#define MZ_STEP_ARGS                                                                                          \
+    b->prm, a.reward, a.value, a.policy, a.beta, a.hsx, a.ne, a.pe, a.K, a.discount, a.pool, a.pool_stride, \
+        a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act
     if (eb && sel)
-        hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, b->prm, a);
+        hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, MZ_STEP_ARGS);
     else if (eb)
-        hipLaunchKernelGGL((k_step<true, false, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, b->prm, a);
+        hipLaunchKernelGGL((k_step<true, false, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream,
+                           MZ_STEP_ARGS);
     else
-        hipLaunchKernelGGL((k_step<false, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, b->prm, a);
+        hipLaunchKernelGGL((k_step<false, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream,
+                           MZ_STEP_ARGS);
+#undef MZ_STEP_ARGS
 }
 
 template <int NC, bool JOINT = false>
@@ -1904,7 +1937,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oQ = o; o += round16(4 * g.P);
     g.oPP = o; o += round16(4 * g.P);
     g.oVs = o; o += round16(4 * g.P);
-    g.oC = o; o += round16(16 * g.PS);
+    g.oC = o; o += round16(16 * g.P);
     g.oPath = o; o += round16(8 * g.PS);
     g.oFlag = o; o += round16(4 * g.PS);
     g.oT = o; o += g.use_table ? round16(4 * g.TT) : 0;
