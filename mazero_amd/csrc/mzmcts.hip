@@ -802,29 +802,34 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         wait_lds();
         if (MZ_STAMPS) bw += __builtin_amdgcn_s_memtime() - w0s;
         const int i = i0 + l;
+        // position of this lane's new (depth, value) among its node's sorted entries: entries of a
+        // smaller depth (lo), of the same depth (c), of the same depth and a smaller value (pv).
+        // Counted by the whole wave, one needing node at a time, 64 entries per ballot.
+        int lo = nv, c = 0, pv = 0;
+        const float key = (l < cnt) ? s.boot[i] : 0.f;
+        for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
+            const int j = __builtin_ctzll(m);
+            const int nvj = rl(nv, j), offj = rl(off, j), depj = D - (i0 + j);
+            const float keyj = rlf(key, j);
+            int cl = 0, cc = 0, cp = 0;
+            for (int e0 = 0; e0 < nvj; e0 += kWave) {
+                const bool on = e0 + l < nvj;
+                const int2 e = on ? s.reg[offj + e0 + l] : make_int2(0x7fffffff, 0);
+                cl += __popcll(ballot(on && e.x < depj));
+                cc += __popcll(ballot(on && e.x == depj));
+                cp += __popcll(ballot(on && e.x == depj && i2f(e.y) < keyj));
+            }
+            if (l == j) {
+                lo = cl;
+                c = cc;
+                pv = cp;
+            }
+            ent_r += nvj;
+        }
+        int pos = 0;
         if (l < cnt) {
             const int dep = D - i;
-            const float key = s.boot[i];
             const int2 *R = s.reg + off;
-            int lo = nv, c = 0, pv = 0;
-            if (need) {
-                lo = 0;
-                int j = 0;
-                for (; j + 4 <= nv; j += 4) {
-                    const int2 e0 = R[j], e1 = R[j + 1], e2 = R[j + 2], e3 = R[j + 3];
-                    lo += (e0.x < dep) + (e1.x < dep) + (e2.x < dep) + (e3.x < dep);
-                    c += (e0.x == dep) + (e1.x == dep) + (e2.x == dep) + (e3.x == dep);
-                    pv += (e0.x == dep && i2f(e0.y) < key) + (e1.x == dep && i2f(e1.y) < key) +
-                          (e2.x == dep && i2f(e2.y) < key) + (e3.x == dep && i2f(e3.y) < key);
-                }
-                for (; j < nv; ++j) {
-                    const int2 e = R[j];
-                    lo += (e.x < dep);
-                    c += (e.x == dep);
-                    pv += (e.x == dep && i2f(e.y) < key);
-                }
-                ent_r += nv;
-            }
             const float4 cw = s.C[n];  // staged per node in round 1
             float ws = cw.x, tw = cw.y;
             const float lp = s.lp[dep];
@@ -854,16 +859,15 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
                     }
                 }
             }
-            // insert (dep, key) at its sorted place: shift the tail up by one in HBM
-            const int pos = lo + pv;
+            // insert (dep, key) at its sorted place (the tail moves up by one below, by the wave)
+            pos = lo + pv;
             int2 *G = gV + (size_t)n * g.E;
             if (nv + 1 > g.E) {
                 err |= kErrPath;
+                pos = nv;  // no shift
             } else {
-                for (int j = nv - 1; j >= pos; --j) G[j + 1] = R[j];
                 G[pos] = make_int2(dep, f2i(key));
             }
-            ent_w += nv - pos + 1;
             // node scalars
             // the leaf's record is being expanded by the other wave: it has children now (nc >= 1),
             // its reward is this simulation's input, and its B record belongs to the expansion
@@ -890,6 +894,15 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
                 d.Q()[gi] = q;
             }
         }
+        // the sorted entries' tails move up by one slot, node by node, 64 entries per store
+        for (unsigned long long m = ballot(l < cnt && nv > pos); m; m &= m - 1ull) {
+            const int j = __builtin_ctzll(m);
+            const int nvj = rl(nv, j), posj = rl(pos, j), offj = rl(off, j), nj = rl(n, j);
+            int2 *Gj = gV + (size_t)nj * g.E;
+            for (int e0 = posj; e0 < nvj; e0 += kWave)
+                if (e0 + l < nvj) Gj[e0 + l + 1] = s.reg[offj + e0 + l];
+        }
+        ent_w += wave_sum((l < cnt) ? (nv - pos + 1) : 0);
         wait_lds();
         i0 += cnt;
         if (i0 <= D) cnt = stage_regions(g, d, s, t, D, i0, n, nv, need, off);
