@@ -80,7 +80,7 @@ struct Geo {
     float one_minus_rho, delta;
     int reg_cap;  // value entries staged in LDS per back-propagation chunk
     // dynamic-LDS byte offsets of k_step
-    int oA, oB, oQ, oPP, oVs, oC, oPath, oFlag, oT, oPb, oSq, oLp, oRng, oBoot, oReg, oX, lds;
+    int oA, oB, oQ, oPP, oVs, oC, oPath, oFlag, oT, oPb, oSq, oLp, oRng, oBoot, oReg, oX, oPar, oSc, lds;
     // agent_num > 1 (joint-action trees, general layout only): agents, N*A, and the LDS regions of
     // the nodes' joint actions [P][N] (bytes), the staged policy / beta / noise [N][A], the
     // per-agent CDFs [N][A] (double) and the draws [K][N]
@@ -93,7 +93,8 @@ struct Dev {
     // 32-bit offsets in 256-byte units keeps the kernel arguments small (each pointer would take
     // two SGPRs for the whole kernel).
     char *base;
-    unsigned o_J, o_A, o_Bn, o_Q, o_PP, o_C, o_D, o_V, o_R, o_hdr, o_path, o_stats, o_err, o_T, o_pb, o_sq, o_lp, o_seed;
+    unsigned o_Par, o_J, o_A, o_Bn, o_Q, o_PP, o_C, o_D, o_V, o_R, o_hdr, o_path, o_stats, o_err, o_T, o_pb, o_sq, o_lp, o_seed;
+    __host__ __device__ int *Par() const { return (int *)(base + (size_t)o_Par * 256); }  // [P] parent index
     __host__ __device__ unsigned char *J() const { return (unsigned char *)(base + (size_t)o_J * 256); }  // [P][N] joint actions (agent_num > 1)
     __host__ __device__ int4 *A() const { return (int4 *)(base + (size_t)o_A * 256); }  // [P] {visit, prior, value, reward}
     __host__ __device__ int4 *Bn() const { return (int4 *)(base + (size_t)o_Bn * 256); }  // [P] {first_child, nc|act<<8|(maxdepth+1)<<16, pred_value, hsx}
@@ -229,6 +230,8 @@ __device__ __forceinline__ int value_lim(int c, float one_minus_rho) {
 struct Lds {
     int4 *A, *B;
     float *Q, *PP, *Vs;
+    int *Par;   // parent index per node (general walks)
+    float *Sc;  // pUCT score of every node under its parent, computed before the walk
     float4 *C;
     int2 *path;
     int *flag;
@@ -265,7 +268,9 @@ struct Layout {
     static constexpr int oBoot = oRng + r16(4 * kRngWin);
     static constexpr int oReg = oBoot + r16(4 * NC);
     static constexpr int oX = oReg + r16(8 * kRegCap);
-    static constexpr int total = oX + r16(8 * (2 * MZ_S_COUNT + 2));
+    static constexpr int oPar = oX + r16(8 * (2 * MZ_S_COUNT + 2));
+    static constexpr int oSc = oPar + r16(4 * NC);
+    static constexpr int total = oSc + r16(4 * NC);
 };
 
 template <int NC>
@@ -288,6 +293,8 @@ __device__ __forceinline__ Lds make_lds(unsigned char *m, const Geo &g) {
         s.rng = (unsigned *)(m + L::oRng);
         s.boot = (float *)(m + L::oBoot);
         s.reg = (int2 *)(m + L::oReg);
+        s.Par = (int *)(m + L::oPar);
+        s.Sc = (float *)(m + L::oSc);
     } else {
         s.A = (int4 *)(m + g.oA);
         s.B = (int4 *)(m + g.oB);
@@ -304,6 +311,8 @@ __device__ __forceinline__ Lds make_lds(unsigned char *m, const Geo &g) {
         s.rng = (unsigned *)(m + g.oRng);
         s.boot = (float *)(m + g.oBoot);
         s.reg = (int2 *)(m + g.oReg);
+        s.Par = (int *)(m + g.oPar);
+        s.Sc = (float *)(m + g.oSc);
     }
     return s;
 }
@@ -368,8 +377,8 @@ __device__ __forceinline__ double cdf_lane(double bd, int A) {
 // Creates the children in HBM (and in the LDS mirrors when given), advances cursor / tot and
 // returns nc.  `pv` is the expanded node's pred_value (the children's PP).
 // --------------------------------------------------------------------------------------------
-__device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float bet, float noi, float eps, int K, float pv,
-                           int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
+__device__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float pol, float bet, float noi, float eps,
+                           int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
                            long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl) {
     const int l = lane_id();
     const int A = g.A;
@@ -432,11 +441,13 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, float pol, float b
         d.D()[gi] = make_float4(pol, bet, bh, 0.f);
         d.Q()[gi] = 0.f;
         d.PP()[gi] = pv;
+        d.Par()[gi] = parent;
         if (s) {
             s->A[c] = a4;
             s->B[c] = b4;
             s->Q[c] = 0.f;
             s->PP[c] = pv;
+            s->Par[c] = parent;
         }
     }
     st_new += nc;
@@ -465,7 +476,8 @@ __device__ __forceinline__ long long rl64(long long v, int j) {
     return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-__device__ int expand_joint(const Geo &g, const Dev &d, int t, const float *pol, const float *bet, const float *noi,
+__device__ int expand_joint(const Geo &g, const Dev &d, int t, int parent, const float *pol, const float *bet,
+                            const float *noi,
                             float eps, int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase,
                             Lds *s, unsigned char *sJ, double *cp, int *draw, int &err, long long &st_new) {
     const int l = lane_id();
@@ -543,6 +555,7 @@ __device__ int expand_joint(const Geo &g, const Dev &d, int t, const float *pol,
         d.D()[gi] = make_float4(pred_prob, beta_prob, bh, 0.f);
         d.Q()[gi] = 0.f;
         d.PP()[gi] = pv;
+        d.Par()[gi] = parent;
         for (int i = 0; i < N; ++i) {
             d.J()[(size_t)t * g.JP + (size_t)c * N + i] = (unsigned char)draw[l * N + i];
             if (sJ) sJ[c * N + i] = (unsigned char)draw[l * N + i];
@@ -552,6 +565,7 @@ __device__ int expand_joint(const Geo &g, const Dev &d, int t, const float *pol,
             s->B[c] = b4;
             s->Q[c] = 0.f;
             s->PP[c] = pv;
+            s->Par[c] = parent;
         }
     }
     st_new += nc;
@@ -648,14 +662,14 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
             jn[i] = a.noise[ib + i];
         }
         wait_lds();
-        nc = expand_joint(g, d, t, jp, jb, jn, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, nullptr, jcp, jd, err,
+        nc = expand_joint(g, d, t, 0, jp, jb, jn, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, nullptr, jcp, jd, err,
                           st_new);
     } else {
         const size_t ib = (size_t)t * A;
         const float pol = (l < A) ? a.policy[ib + l] : 0.f;
         const float bet = (l < A) ? a.beta[ib + l] : 0.f;
         const float noi = (l < A) ? a.noise[ib + l] : 0.f;
-        nc = expand_node(g, d, t, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false, 0u,
+        nc = expand_node(g, d, t, 0, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false, 0u,
                          0u, nullptr);
     }
     if (l == 0) {
@@ -966,6 +980,12 @@ __device__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const Tr
             if (vs < 0) vs = 0;
             if (vs > 1) vs = 1;
             s.Vs[n] = vs;
+            if (g.K > 1 && n >= 1) {
+                // ucb_score under the parent (cnode.cpp:297-335), as the walk would compute it;
+                // a parent outside the pUCT table range is reported by the walk itself
+                const int np = s.A[s.Par[n]].x - 1;  // total_children_visit_counts
+                s.Sc[n] = (np >= 0 && np < g.PS) ? puct(g, s, np, a4.x) * i2f(a4.y) + vs : 0.f;
+            }
         }
     }
     wait_lds();
@@ -1052,7 +1072,15 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 
     int x = 0, D = 0, cursor = cursor0, phsx = 0;
     int4 xa = make_int4(0, 0, 0, 0), xb = xa;
+#ifdef MZ_PROBE3
+    const unsigned long long q0 = __builtin_amdgcn_s_memtime();
+    unsigned long long q1 = q0, q2 = q0;
+    int attempts = 0;
+#endif
     for (int attempt = 0; attempt < 2; ++attempt) {
+#ifdef MZ_PROBE3
+        ++attempts;
+#endif
         const bool spec = (attempt == 0);
         x = 0;
         D = 0;
@@ -1095,7 +1123,7 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
                     break;
                 }
                 float sc = -INFINITY;
-                if (has) sc = puct(g, s, ntot, ca.x) * i2f(ca.y) + vsl;
+                if (has) sc = s.Sc[fc + l];  // puct(ntot, visit) * prior + value score, precomputed
                 scored += nc;
                 const float M = wave_max(sc);
                 unsigned long long lst;
@@ -1130,6 +1158,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
                 s.flag[D] = fl;
             }
         }
+#ifdef MZ_PROBE3
+        q1 = __builtin_amdgcn_s_memtime();
+#endif
         if (!spec) break;
         // verify the speculated single-child levels in parallel
         wait_lds();
@@ -1155,6 +1186,13 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
     stl[MZ_S_PATH_EDGES] += D;
     stl[MZ_S_SCORED] += scored;
     wait_lds();
+#ifdef MZ_PROBE3
+    q2 = __builtin_amdgcn_s_memtime();
+    stl[MZ_S_CYC_W1_ROUND1] += (long long)(q1 - q0);   // walk (last attempt's descent)
+    stl[MZ_S_CYC_W1_STAGE2] += (long long)(q2 - q1);   // speculation check
+    stl[MZ_S_CYC_W1_BACKUP] += attempts;               // attempts (2 = re-walk)
+    stl[MZ_S_CYC_W1_SYNC] += D;
+#endif
     // publish the path {node, visit} for the next back-propagation
     int2 *gp = d.path() + (size_t)t * g.PS;
     for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
@@ -1175,6 +1213,10 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
                                               const float *policy, const float *beta, int hsx, int ne, int pe, int K,
                                               float discount, const char *pool, long long pool_stride,
                                               long long row_bytes, char *gather_out, int *idx_x, int *idy, int *act) {
+#ifdef MZ_PROBE2
+    unsigned long long pt0;
+    asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(pt0)::"memory");
+#endif
     const Geo g = prm->g;
     const Dev d = prm->d;
     StepArgs a;
@@ -1272,6 +1314,7 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
                 glds16(d.A() + nb + i0 + l, s.A + i0);
                 glds16(d.Bn() + nb + i0 + l, s.B + i0);
                 glds4(d.PP() + nb + i0 + l, s.PP + i0);
+                if (SEL && g.K > 1) glds4(d.Par() + nb + i0 + l, s.Par + i0);  // parents (general walk)
                 if (EB) {
                     glds4(d.Q() + nb + i0 + l, s.Q + i0);
                     glds16(d.C() + nb + i0 + l, s.C + i0);  // value-set scalars, read by node
@@ -1342,6 +1385,7 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
                 glds16(d.A() + nb + i0 + l, s.A + i0);
                 glds16(d.Bn() + nb + i0 + l, s.B + i0);
                 glds4(d.PP() + nb + i0 + l, s.PP + i0);
+                if (SEL && g.K > 1) glds4(d.Par() + nb + i0 + l, s.Par + i0);
                 if (EB) {
                     glds4(d.Q() + nb + i0 + l, s.Q + i0);
                     glds16(d.C() + nb + i0 + l, s.C + i0);
@@ -1388,10 +1432,10 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
             long long st_new = 0;
             int nc;
             if (JOINT)
-                nc = expand_joint(g, d, t, sJpol, sJbet, nullptr, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, sJ,
+                nc = expand_joint(g, d, t, leaf, sJpol, sJbet, nullptr, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, sJ,
                                   (double *)(smem + g.oJcp), (int *)(smem + g.oJdraw), err, st_new);
             else
-                nc = expand_node(g, d, t, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new,
+                nc = expand_node(g, d, t, leaf, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new,
                                  have_w, w1r, w2r, stl);
             stl[MZ_S_EXPANDS] += 1;
             stl[MZ_S_NEW_CHILDREN] += st_new;
@@ -1410,7 +1454,11 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
             stamp(ts, 4);
             backup(g, d, s, t, h.D, tot, v_in, r_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl);
             stamp(ts, 5);
+#if defined(MZ_PROBE2) || defined(MZ_PROBE3)
+            if (false) {
+#else
             if (MZ_STAMPS && SEL) {
+#endif
                 stl[MZ_S_CYC_W1_ROUND1] += (long long)(ts[1] - ts[0]);
                 stl[MZ_S_CYC_W1_STAGE2] += (long long)(ts[3] - ts[2]);
                 stl[MZ_S_CYC_W1_BACKUP] += (long long)(ts[5] - ts[4]);
@@ -1455,7 +1503,13 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
     wait_vm();  // RNG window (and anything staged) has landed
     stamp(ts, 6);
     if (SEL && !err) {
+#ifdef MZ_PROBE3
+        const unsigned long long v0 = __builtin_amdgcn_s_memtime();
+#endif
         value_scores(g, s, h.tot, a.discount, h);
+#ifdef MZ_PROBE3
+        stl[MZ_S_CYC_EXP_CDF] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // value scores
+#endif
         // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
         int perr = 0;  // words past the stream end only matter if the walk consumes them
         const unsigned rw0 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
@@ -1537,6 +1591,16 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
         stl[MZ_S_CYC_W1_STAGE2] = (long long)(pr1 - pr0);     // T table issue
         stl[MZ_S_CYC_W1_BACKUP] = (long long)(pr2 - pr1);     // inputs + header issue
         stl[MZ_S_CYC_W1_SYNC] = (long long)(ts[1] - pr2);     // wait for round 1
+    }
+#endif
+#ifdef MZ_PROBE2
+    if (EB && SEL && !err) {
+        unsigned long long pt1;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(pt1)::"memory");
+        stl[MZ_S_CYC_W1_ROUND1] = (long long)(ts[0] - pt0);  // kernel entry -> first stamp
+        stl[MZ_S_CYC_W1_STAGE2] = (long long)(pt1 - pt0);    // whole wave-0 span incl. store drain
+        stl[MZ_S_CYC_W1_BACKUP] = (long long)(pt1 - ts[9]);  // store drain after the last stamp
+        stl[MZ_S_CYC_W1_SYNC] = 0;
     }
 #endif
     if (MZ_STAMPS && EB && SEL && !err) {
@@ -1961,6 +2025,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oBoot = o; o += round16(4 * g.PS);
     g.oReg = o; o += round16(8 * g.reg_cap);
     g.oX = o; o += round16(8 * (2 * MZ_S_COUNT + 2));
+    g.oPar = o; o += round16(4 * g.P);
+    g.oSc = o; o += round16(4 * g.P);
     g.N = N;
     g.NA = N * A;
     g.JP = (N > 1) ? round16(b->P * N) : 0;
@@ -2019,6 +2085,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         plan.dev<float>(d.o_pb, (size_t)b->PS + kWave);
         plan.dev<double>(d.o_sq, (size_t)b->PS + kWave);
         plan.dev<int4>(d.o_A, nodes);
+        plan.dev<int>(d.o_Par, nodes);
         plan.dev<int4>(d.o_Bn, nodes);
         plan.dev<float>(d.o_Q, nodes);
         plan.dev<float>(d.o_PP, nodes);
