@@ -88,11 +88,20 @@ struct Geo {
     int oJ, oJpol, oJbet, oJcp, oJdraw;
 };
 
+#ifdef __HIP_DEVICE_COMPILE__
+typedef __attribute__((address_space(1))) char gchar;
+#else
+typedef char gchar;
+#endif
+
 struct Dev {
     // Every array lives in one device allocation (the handle's arena): a base pointer plus
     // 32-bit offsets in 256-byte units keeps the kernel arguments small (each pointer would take
     // two SGPRs for the whole kernel).
-    char *base;
+    // On the device the arena pointer is typed as global memory, so every access through it is a
+    // global_* op: a flat_* op also counts against lgkmcnt, and every LDS wait after it would wait
+    // for the HBM access too (outstanding write-backs included).
+    gchar *base;
     unsigned o_Par, o_J, o_A, o_Bn, o_Q, o_PP, o_C, o_D, o_V, o_R, o_hdr, o_path, o_stats, o_err, o_T, o_pb, o_sq, o_lp, o_seed;
     __host__ __device__ int *Par() const { return (int *)(base + (size_t)o_Par * 256); }  // [P] parent index
     __host__ __device__ unsigned char *J() const { return (unsigned char *)(base + (size_t)o_J * 256); }  // [P][N] joint actions (agent_num > 1)
@@ -1094,6 +1103,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
             s.flag[0] = 0;
         }
         while (true) {
+#ifdef MZ_PROBE3
+            const unsigned long long lv0 = __builtin_amdgcn_s_memtime();
+#endif
             x = uni(x);
             D = uni(D);
             cursor = uni(cursor);
@@ -1104,12 +1116,15 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
             const int fc = xb.x;
             const bool has = l < nc;
             int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
-            float vsl = 0.f;
             if (has) {
                 ca = s.A[fc + l];
                 cb = s.B[fc + l];
-                vsl = s.Vs[fc + l];
             }
+#ifdef MZ_PROBE3
+            wait_lds();
+            const unsigned long long lv1 = __builtin_amdgcn_s_memtime();
+            stl[MZ_S_CYC_W1_ROUND1] += (long long)(lv1 - lv0);  // level head: uniform state + children reads
+#endif
             int ci = 0, fl = 0;
             if (x == 0 && xa.x <= nc) {
                 ci = xa.x - 1;  // forced root round-robin (cnode.cpp:398-399)
@@ -1122,9 +1137,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
                     err |= kErrTable;
                     break;
                 }
+                scored += nc;
                 float sc = -INFINITY;
                 if (has) sc = s.Sc[fc + l];  // puct(ntot, visit) * prior + value score, precomputed
-                scored += nc;
                 const float M = wave_max(sc);
                 unsigned long long lst;
                 if (M > -1000000.0f) {
@@ -1144,6 +1159,10 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
                 }
             }
             // descend
+#ifdef MZ_PROBE3
+            const unsigned long long lv2 = __builtin_amdgcn_s_memtime();
+            stl[MZ_S_CYC_W1_STAGE2] += (long long)(lv2 - lv1);  // score, arg-max, tie word
+#endif
             phsx = xb.w;
             x = fc + ci;
             xa = make_int4(rl(ca.x, ci), rl(ca.y, ci), rl(ca.z, ci), rl(ca.w, ci));
@@ -1157,6 +1176,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
                 s.path[D] = make_int2(x, xa.x);
                 s.flag[D] = fl;
             }
+#ifdef MZ_PROBE3
+            stl[MZ_S_CYC_W1_BACKUP] += (long long)(__builtin_amdgcn_s_memtime() - lv2);  // descend
+#endif
         }
 #ifdef MZ_PROBE3
         q1 = __builtin_amdgcn_s_memtime();
@@ -1188,10 +1210,9 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
     wait_lds();
 #ifdef MZ_PROBE3
     q2 = __builtin_amdgcn_s_memtime();
-    stl[MZ_S_CYC_W1_ROUND1] += (long long)(q1 - q0);   // walk (last attempt's descent)
-    stl[MZ_S_CYC_W1_STAGE2] += (long long)(q2 - q1);   // speculation check
-    stl[MZ_S_CYC_W1_BACKUP] += attempts;               // attempts (2 = re-walk)
-    stl[MZ_S_CYC_W1_SYNC] += D;
+    stl[MZ_S_CYC_EXP_DRAW] += (long long)(q1 - q0);    // walk (last attempt's descent)
+    stl[MZ_S_CYC_EXP_NODES] += (long long)(q2 - q1);   // speculation check
+    stl[MZ_S_CYC_W1_SYNC] += attempts + 100 * D;
 #endif
     // publish the path {node, visit} for the next back-propagation
     int2 *gp = d.path() + (size_t)t * g.PS;
@@ -1839,7 +1860,7 @@ struct ArenaPlan {
         void *q = nullptr;
         HIP_TRY(hipMalloc(&q, total));
         b->allocs.push_back(q);
-        d.base = (char *)q;
+        d.base = (gchar *)q;
         for (auto &r : req) {
             if (r.off) *r.off = (unsigned)(r.at / 256);
             else *r.ptr = (char *)q + r.at;
