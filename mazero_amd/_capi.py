@@ -1,4 +1,5 @@
-"""ctypes binding of the C-ABI declared in include/mzmcts.h and include/mzdriver.h.
+"""ctypes binding of the C-ABI declared in include/mzmcts.h, include/mzdriver.h and
+include/mzconsume.h.
 
 `bind(lib)` declares argument/return types on any shared library exporting that ABI.  The product
 loads its own HIP library through `mazero_amd._lib.load()`; the tests use the same binder on the
@@ -99,6 +100,15 @@ DRIVER_SIGNATURES = {
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 
+# include/mzconsume.h (on-device consumers of the search output; product library only)
+MZ_MARGINAL_GIVEN, MZ_MARGINAL_ARGMAX = 0, 1
+CONSUME_SIGNATURES = {
+    "mz_select_actions": (_i, [_p, _p, _p, _p, _i, C.c_double, _i, _p, _p, _p, _p]),
+    "mz_eps_greedy": (_i, [_p, _p, _i64, _f, _p, _p, _p]),
+    "mz_marginal_policy": (_i, [_p, _p, _i64, _p, _i64, _i, _p, _p, _p]),
+}
+CONSUME_EXPORTS = sorted(CONSUME_SIGNATURES)
+
 
 def bind(lib: C.CDLL) -> C.CDLL:
     sig = {
@@ -129,6 +139,7 @@ def bind(lib: C.CDLL) -> C.CDLL:
     }
     if hasattr(lib, "mz_policy_glue"):  # include/mzdriver.h: product library only
         sig.update(DRIVER_SIGNATURES)
+        sig.update(CONSUME_SIGNATURES)
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res

@@ -17,7 +17,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", "mzmcts.hip"), os.path.join(HERE, "csrc", "mzdriver.hip")]
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("mzmcts.hip", "mzdriver.hip", "mzconsume.hip")]
 SRC = SRCS[0]
 OUT_DIR = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT_DIR, "libmzmcts.so")
@@ -53,7 +53,7 @@ def needs_build(lib: str = LIB) -> bool:
         return True
     t = os.path.getmtime(lib)
     deps = [*SRCS, os.path.join(HERE, "csrc", "mz_internal.h"), os.path.join(ROOT, "include", "mzmcts.h"),
-            os.path.join(ROOT, "include", "mzdriver.h"), __file__]
+            os.path.join(ROOT, "include", "mzdriver.h"), os.path.join(ROOT, "include", "mzconsume.h"), __file__]
     return any(os.path.getmtime(p) > t for p in deps)
 
 

@@ -1,5 +1,5 @@
-// mz_internal.h — what the driver-glue translation unit (mzdriver.hip) needs from the tree
-// library (mzmcts.hip).  Hidden symbols: not part of the C-ABI.
+// mz_internal.h — what the driver-glue and consumer translation units (mzdriver.hip,
+// mzconsume.hip) need from the tree library (mzmcts.hip).  Hidden symbols: not part of the C-ABI.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -12,4 +12,6 @@ extern "C" {
 MZ_HIDDEN int mz_internal_fail(int code, const char *msg);
 // Make the handle's device current and report its batch size, action count and stream.
 MZ_HIDDEN int mz_internal_launch_info(mz_batch *b, int *B, int *A, hipStream_t *stream);
+// agent_num of the handle (0 for a null handle).
+MZ_HIDDEN int mz_internal_agent_num(mz_batch *b);
 }  // extern "C"

@@ -2361,6 +2361,8 @@ int mz_internal_launch_info(mz_batch *b, int *B, int *A, hipStream_t *stream) {
     return MZ_OK;
 }
 
+int mz_internal_agent_num(mz_batch *b) { return b ? b->N : 0; }
+
 int mz_gather_rows(mz_batch *b, const void *pool, int64_t stride, int64_t row_bytes, const int32_t *idx_x, void *out) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
     if (row_bytes <= 0 || (row_bytes & 3)) return fail(MZ_ERR_ARG, "row_bytes must be a positive multiple of 4");

@@ -69,6 +69,7 @@ class DeviceSearchOutput(NamedTuple):
     marginal_priors: torch.Tensor        # f32 [B, 1, A]
     degrees: torch.Tensor                # i32 [B]
     sampled: dict                        # field -> [B, maxdeg] (i32 for actions / visit_count)
+    tree: object = None                  # the Tree_batch that ran the search (its stream; consumers)
 
     def to_host(self) -> SearchOutput:
         deg = self.degrees.cpu().numpy()
@@ -126,7 +127,10 @@ class _SearchLoop:
         for t, a in zip(self.rin, root_arrays):
             t.copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
         if self.cur > 0:
-            self.fac.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(factor)[:, : self.cur], dtype=np.int32)))
+            if isinstance(factor, torch.Tensor):  # previous agents' actions, already on the device
+                self.fac.copy_(factor[:, : self.cur])
+            else:
+                self.fac.copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(factor)[:, : self.cur], dtype=np.int32)))
 
     def run(self, model, cfg, eps, tau):
         """One search, mcts_sampled.py:106-172, all on the current stream."""
@@ -310,7 +314,7 @@ class SampledMCTS:
             sampled = {}
             for f in _SAMPLED_FIELDS:
                 sampled[f], _ = tb.get_roots_sampled_padded_device(f, disc, degrees_out=deg if f == "actions" else None)
-            return DeviceSearchOutput(value, mv, mp, deg, sampled)
+            return DeviceSearchOutput(value, mv, mp, deg, sampled, tb)
 
     @staticmethod
     def _recurrent(model, hidden, action):

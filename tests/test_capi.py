@@ -1,7 +1,8 @@
 """The C-ABI boundary (CPU only: no device compute here).
 
 * every entry point declared in include/mzmcts.h is exported by the product library and by both
-  oracle libraries; include/mzdriver.h (driver glue) by the product library
+  oracle libraries; include/mzdriver.h (driver glue) and include/mzconsume.h (consumers) by the
+  product library
 * the product library loads on a machine without a GPU and fails loudly (no silent fallback)
 * the Tree_batch shim mirrors cytree.pyx's argument handling (dtype check -> ValueError,
   invariant violations -> RuntimeError)
@@ -22,6 +23,7 @@ from mazero_amd.cytree import Tree_batch
 
 HEADER = os.path.join(ROOT, "include", "mzmcts.h")
 DRIVER_HEADER = os.path.join(ROOT, "include", "mzdriver.h")
+CONSUME_HEADER = os.path.join(ROOT, "include", "mzconsume.h")
 
 
 def declared_symbols(header=HEADER):
@@ -38,6 +40,16 @@ def test_driver_header_matches_binding_table():
         assert hasattr(raw, name), name
     # internal hooks of the driver TU stay hidden
     assert not hasattr(raw, "mz_internal_fail")
+    assert not hasattr(raw, "mz_internal_agent_num")
+
+
+def test_consume_header_matches_binding_table():
+    assert declared_symbols(CONSUME_HEADER) == _capi.CONSUME_EXPORTS
+    from mazero_amd import build
+
+    raw = C.CDLL(build.build(verbose=False))
+    for name in _capi.CONSUME_EXPORTS:
+        assert hasattr(raw, name), name
 
 
 def test_header_matches_binding_table():
