@@ -41,6 +41,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+import mazero_amd  # noqa: E402,F401  (HIP runtime settings, before anything initialises HIP)
 
 CONFIGS = {  # name: (agents N, actions A) -- smac_maps.py:17-133, n_actions = 6 + n_enemies
     "3m": (3, 9),

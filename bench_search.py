@@ -10,6 +10,10 @@ Reported, as one JSON line:
 - `device`: mazero_amd.mcts_sampled.SampledMCTS. The tree, pool and glue are on the GPU, and
   the search loop is captured in a HIP graph after the first search of each configuration.
 - `device_eager`: the same driver without graphs.
+- `selfplay_step_host_consumers` / `selfplay_step_device_consumers`: a whole self-play step with
+  its per-root decisions (select_action, epsilon-greedy, recorded policy probability,
+  selfplay_worker.py:189-293) made by the reference's Python on the host (oracle/consume.py) or
+  by the device consumers (mazero_amd.consume); both on the `device` search.
 - `reference_loop` (when oracle/_ref is built): the reference driver restated in
   oracle/driver.py, i.e. numpy glue, vstack gathers and the reference C++ ctree on one host
   core, driving the same GPU network. This is what a reference self-play step costs on this
@@ -30,6 +34,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+import mazero_amd  # noqa: E402,F401  (HIP runtime settings, before anything initialises HIP)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 MAPS = {"3m": (3, 9), "2s3z": (5, 11), "3s5z_vs_3s6z": (8, 15), "27m_vs_30m": (27, 36)}
@@ -86,6 +91,49 @@ def main():
     line["device"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3)}
     t = timed(SampledMCTS(cfg, np.random.RandomState(0), use_graph=False), max(1, args.steps // 2), 1)
     line["device_eager"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3)}
+
+    # One whole self-play step (selfplay_worker.py:189-293): the agents' searches plus the per-root
+    # decisions (select_action, epsilon-greedy, recorded policy probability), with the decisions
+    # made by the reference's Python on the host or by the device consumers (mazero_amd.consume).
+    from consume import selfplay_step
+    from mazero_amd.consume import selfplay_decisions
+
+    class _DictSearch(SampledMCTS):
+        def batch_search(self, *a, **k):
+            return super().batch_search(*a, **k)._asdict()
+
+    ur = np.random.default_rng(1)
+    u_eps, u_cat = ur.random((N, B)).astype(np.float32), ur.random((N, B))
+
+    def timed_step(fn, steps, warm):
+        for i in range(warm):
+            fn(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / steps
+
+    rs_h, rs_d = np.random.default_rng(3), np.random.default_rng(3)
+    m_h, m_d = _DictSearch(cfg, rs_h), SampledMCTS(cfg, rs_d)
+
+    def host_decisions(i):
+        out, legal = roots[i % len(roots)]
+        return selfplay_step(m_h, net, out, N, legal, 1.0, 1.0, 0.1, rs_h, u_eps, u_cat, device=dev)["actions"]
+
+    def device_decisions(i):
+        out, legal = roots[i % len(roots)]
+        d = selfplay_decisions(m_d, net, out, N, legal, temperature=1.0, greedy_epsilon=0.1,
+                               eps_uniforms=(u_eps, u_cat), device=dev)
+        return d.actions.cpu().numpy()  # the environment step needs the actions on the host
+
+    same_dec = bool(np.array_equal(host_decisions(0), device_decisions(0)))
+    t = timed_step(host_decisions, args.steps, 1)
+    line["selfplay_step_host_consumers"] = {"ms_per_step": round(t * 1e3, 3), "value": round(sims_per_step / t, 1)}
+    t = timed_step(device_decisions, args.steps, 1)
+    line["selfplay_step_device_consumers"] = {"ms_per_step": round(t * 1e3, 3), "value": round(sims_per_step / t, 1),
+                                              "actions_equal_host_consumers": same_dec}
 
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libmzref.so")
     if not args.no_ref and os.path.exists(ref_path):

@@ -27,12 +27,14 @@ Model interface (core/model.py:45-79): `prediction(h) -> (policy_logits [B,N,A],
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 import weakref
 from typing import List, NamedTuple, Tuple
 
 import numpy as np
 import torch
 
+from . import _hipenv
 from ._capi import MZ_DT_F16, MZ_DT_F32, check
 from .cytree import Tree_batch
 
@@ -200,6 +202,10 @@ class SampledMCTS:
         self.config = config
         self.np_random = np.random if np_random is None else np_random
         self._lib = lib
+        if use_graph and not _hipenv.GRAPHS_SAFE:
+            warnings.warn("HIP was initialised before mazero_amd was imported without "
+                          "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0: search graphs are disabled (see mazero_amd/_hipenv.py)")
+            use_graph = False
         self.use_graph = use_graph
 
     # ---------------------------------------------------------------------------------------

@@ -19,6 +19,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import mazero_amd  # noqa: E402,F401  (HIP runtime settings, before anything initialises HIP)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")

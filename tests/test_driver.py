@@ -320,3 +320,55 @@ def test_driver_graph_replay_matches_oracle(K, port_lib):
         exp = oracle.batch_search(net, out, cur, factor, N, legal, device=dev, add_noise=True)
         got = drv.batch_search(net, out, cur, factor, N, legal, device=dev, add_noise=True)
         _compare_outputs(got, exp)
+
+
+@pytest.mark.gpu
+def test_graph_replay_after_eager_launches(port_lib):
+    """A captured search graph replayed after thousands of ordinary launches (eager searches of the
+    same configuration) still matches the oracle.  With the HIP runtime's graph packet capture on
+    (DEBUG_CLR_GRAPH_PACKET_CAPTURE unset or 1) this exact sequence failed in agent 1's replay:
+    mazero_amd/_hipenv.py."""
+    import torch
+
+    from consume import eps_greedy_given, select_action
+    from driver import OracleSampledMCTS
+    from mazero_amd import _hipenv
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    assert _hipenv.GRAPHS_SAFE
+    N, A, B, S = 3, 9, 256, 50
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=1)
+    net = make_net(N, A, seed=0, device=dev)
+    roots = [make_root_batch(net, B, 64, seed=10 + i, device=dev, legal_zero_frac=0.2) for i in range(3)]
+    for n_steps, use_graph in ((7, True), (3, False)):  # graph captures + replays, then eager searches
+        m = SampledMCTS(cfg, np.random.RandomState(0), use_graph=use_graph)
+        for i in range(n_steps):
+            out, legal = roots[i % 3]
+            acts = np.zeros((B, N), np.int32)
+            for agent in range(N):
+                r = m.batch_search(net, out, agent, acts[:, :agent].copy() if agent else None, N, legal, device=dev,
+                                   add_noise=True)
+                acts[:, agent] = [int(a[np.argmax(v), 0]) for a, v in zip(r.sampled_actions, r.sampled_visit_count)]
+    # a self-play step replaying the graphs, against the oracle driver
+    ur = np.random.default_rng(1)
+    u_eps, u_cat = ur.random((N, B)).astype(np.float32), ur.random((N, B))
+    rs_o, rs_d = np.random.default_rng(3), np.random.default_rng(3)
+    oracle, drv = OracleSampledMCTS(cfg, rs_o, port_lib), SampledMCTS(cfg, rs_d)
+    out, legal = roots[0]
+    acts = np.full((B, N), -1, np.int32)
+    got, factors = [], []
+    for agent in range(N):  # the device step first: the oracle's eager network calls would move the launch ring
+        factors.append(acts[:, :agent].copy() if agent else None)
+        got.append(drv.batch_search(net, out, agent, factors[-1], N, legal, device=dev, add_noise=True))
+        for i in range(B):
+            pos, _ = select_action(got[-1].sampled_visit_count[i], 1.0, False, rs_d)
+            acts[i, agent] = eps_greedy_given(got[-1].sampled_actions[i][pos, 0], legal[i, agent], 0.1,
+                                              u_eps[agent, i], u_cat[agent, i])
+    for agent in range(N):
+        exp = oracle.batch_search(net, out, agent, factors[agent], N, legal, device=dev, add_noise=True)
+        _compare_outputs(got[agent], exp)
+        for i in range(B):
+            select_action(exp["sampled_visit_count"][i], 1.0, False, rs_o)
+    assert rs_o.random() == rs_d.random()
