@@ -19,7 +19,7 @@ step() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS} ;;
+    pytest) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS} ;;
     search) step bench_search 900 python bench_search.py ${SEARCH_ARGS} ;;
