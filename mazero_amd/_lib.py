@@ -26,7 +26,7 @@ def load() -> C.CDLL:
             return _lib
         path = LIB_STAMPS if os.environ.get("MZ_STAMPS") == "1" else LIB
         # experiment builds of the same source (scripts/, diagnostics only)
-        path = os.environ.get("MZ_LIB_OVERRIDE", path)
+        path = os.environ.get("MZ_LIB_OVERRIDE") or path
         try:
             import torch  # noqa: F401  (plumbing: share torch's HIP runtime)
         except Exception:

@@ -68,6 +68,10 @@ struct TreeHdr {
     int cursor, tot, D, err;
     float mm_min, mm_max;
     int mm_cnt, leaf;
+    // 1 while every reward and pred_value of the tree lies in [-1e30, 1e30] and every prior in
+    // [0, 1e30]: then (with the handle's fast_ok conditions) no pUCT score can be NaN or below
+    // FLOAT_MIN, so a K = 1 selection consumes one engine word per non-forced level (select_walk)
+    int tame;
     unsigned nxt[kNxt];  // R[cursor .. cursor + kNxt): the next expansion's engine words
 };
 
@@ -151,6 +155,39 @@ struct Params {
     Dev d;
 };
 
+// Arena offsets of every array a k_step launch reads in its first round, as a function of the
+// geometry alone (B, P, PS): mz_create's ArenaPlan requests the arrays in exactly this order and
+// checks the result against this function, so the kernel computes these addresses from its
+// preloaded SGPR arguments and its first loads do not wait for the Params block.
+__host__ __device__ __forceinline__ unsigned long long arena_span(unsigned long long bytes) {
+    return (bytes + 64 + 255) / 256;  // ArenaPlan::span, in 256-byte units
+}
+__host__ __device__ __forceinline__ void arena_hot(Dev &d, long long B, long long P, long long PS) {
+    const unsigned long long nodes = (unsigned long long)B * P;
+    const unsigned long long TT = (unsigned long long)(((PS * (PS + 1) / 2) + 3) & ~3ll);
+    unsigned long long o = arena_span(sizeof(Params));
+    d.o_hdr = (unsigned)o; o += arena_span((unsigned long long)B * sizeof(TreeHdr));
+    d.o_stats = (unsigned)o; o += arena_span((unsigned long long)B * MZ_S_COUNT * 8);
+    d.o_err = (unsigned)o; o += arena_span(4);
+    d.o_seed = (unsigned)o; o += arena_span(4);
+    d.o_lp = (unsigned)o; o += arena_span(4 * ((unsigned long long)PS + 1 + kWave));
+    d.o_T = (unsigned)o; o += arena_span(4 * (TT + 4 * kWave));
+    d.o_pb = (unsigned)o; o += arena_span(4 * ((unsigned long long)PS + kWave));
+    d.o_sq = (unsigned)o; o += arena_span(8 * ((unsigned long long)PS + kWave));
+    d.o_A = (unsigned)o; o += arena_span(16 * nodes);
+    d.o_Par = (unsigned)o; o += arena_span(4 * nodes);
+    d.o_Bn = (unsigned)o; o += arena_span(16 * nodes);
+    d.o_Q = (unsigned)o; o += arena_span(4 * nodes);
+    d.o_PP = (unsigned)o; o += arena_span(4 * nodes);
+    d.o_C = (unsigned)o; o += arena_span(16 * nodes);
+    d.o_path = (unsigned)o;
+}
+
+#ifdef __HIP_DEVICE_COMPILE__
+typedef const __attribute__((address_space(4))) Params cParams;
+#else
+typedef const Params cParams;
+#endif
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
 
@@ -227,6 +264,9 @@ __device__ __forceinline__ int wave_sum(int v) {
     return rl(v, 0) + rl(v, 16) + rl(v, 32) + rl(v, 48);
 }
 
+__device__ __forceinline__ bool tame_val(float x) { return x >= -1e30f && x <= 1e30f; }  // false for NaN
+__device__ __forceinline__ bool tame_prior(float x) { return x >= 0.f && x <= 1e30f; }
+
 // size_lim of SubTreeValueSet::update (utils.cpp:31): max(1, (int)ceil(count * (1 - rho)))
 __device__ __forceinline__ int value_lim(int c, float one_minus_rho) {
     const int v = (int)ceilf((float)c * one_minus_rho);
@@ -275,7 +315,7 @@ struct Layout {
     static constexpr int oLp = oSq + r16(8 * (NC + kWave));
     static constexpr int oRng = oLp + r16(4 * (NC + 1 + kWave));
     static constexpr int oBoot = oRng + r16(4 * kRngWin);
-    static constexpr int oReg = oBoot + r16(4 * NC);
+    static constexpr int oReg = oBoot + r16(4 * (NC + kWave));
     static constexpr int oX = oReg + r16(8 * kRegCap);
     static constexpr int oPar = oX + r16(8 * (2 * MZ_S_COUNT + 2));
     static constexpr int oSc = oPar + r16(4 * NC);
@@ -349,23 +389,51 @@ __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, co
 // sum, p = w / sum, sequential prefix sums, the last forced to 1.0.  Returns this lane's cumulative
 // probability.  Serial chains in blocks of 8 fully unrolled steps (readlane is convergent, so the
 // compiler cannot unroll a runtime-count loop over it by itself).
+// v = (bit l of m) ? x : v for this lane l, with m built by the scalar unit (one v_cndmask per
+// dword, no VALU compare)
+__device__ __forceinline__ float sel_lane(float v, float x, unsigned long long m) {
+    asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(v) : "v"(x), "s"(m));
+    return v;
+}
+__device__ __forceinline__ double sel_lane(double v, double x, unsigned long long m) {
+    const long long vb = __double_as_longlong(v), xb = __double_as_longlong(x);
+    const float lo = sel_lane(__int_as_float((int)(unsigned)(vb & 0xffffffffll)),
+                              __int_as_float((int)(unsigned)(xb & 0xffffffffll)), m);
+    const float hi = sel_lane(__int_as_float((int)(vb >> 32)), __int_as_float((int)(xb >> 32)), m);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)__float_as_int(hi) << 32) |
+                                            (unsigned)__float_as_int(lo)));
+}
+
 __device__ __forceinline__ double cdf_lane(double bd, int A) {
     const int l = lane_id();
+    // Both chains read their operands into SGPRs 8 at a time ahead of the dependent adds (a
+    // v_readlane result consumed right away by a VALU stalls the chain); lane a keeps its prefix
+    // sum through v_cndmask on a SALU-built lane mask.
     double sum = 0.0;
     int a0 = 0;
     for (; a0 + 8 <= A; a0 += 8) {
+        double w8[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sum += rld(bd, a0 + j);
+        for (int j = 0; j < 8; ++j) w8[j] = rld(bd, a0 + j);
+        asm volatile("" : "+s"(w8[0]), "+s"(w8[1]), "+s"(w8[2]), "+s"(w8[3]), "+s"(w8[4]), "+s"(w8[5]),
+                     "+s"(w8[6]), "+s"(w8[7]));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += w8[j];
     }
     for (; a0 < A; ++a0) sum += rld(bd, a0);
     const double p = bd / sum;
     double acc = rld(p, 0), cp = (l == 0) ? acc : 0.0;
     a0 = 1;
     for (; a0 + 8 <= A; a0 += 8) {
+        double p8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) p8[j] = rld(p, a0 + j);
+        asm volatile("" : "+s"(p8[0]), "+s"(p8[1]), "+s"(p8[2]), "+s"(p8[3]), "+s"(p8[4]), "+s"(p8[5]),
+                     "+s"(p8[6]), "+s"(p8[7]));
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            acc = acc + rld(p, a0 + j);
-            cp = (l == a0 + j) ? acc : cp;
+            acc = acc + p8[j];
+            cp = sel_lane(cp, acc, 1ull << (a0 + j));
         }
     }
     for (; a0 < A; ++a0) {
@@ -388,7 +456,7 @@ __device__ __forceinline__ double cdf_lane(double bd, int A) {
 // --------------------------------------------------------------------------------------------
 __device__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float pol, float bet, float noi, float eps,
                            int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
-                           long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl) {
+                           long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl, int &wild) {
     const int l = lane_id();
     const int A = g.A;
     int cnt = 0;  // number of draws that hit action l
@@ -441,6 +509,7 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float 
         const float bh = (float)cnt / (float)K;  // betahat_prob = count / sampled_times
         float prior = (eps > 0) ? (pol * (1 - eps) + noi * eps) : pol;
         prior = prior * bh / bet;  // prior * betahat_prob / beta_prob
+        if (!tame_prior(prior)) wild = 1;
         const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
         const int4 b4 = make_int4(0, pack_y(0, l, -1), f2i(0.0f), -1);
         const size_t gi = (size_t)t * g.P + c;
@@ -459,6 +528,7 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float 
             s->Par[c] = parent;
         }
     }
+    wild = (ballot(wild != 0) != 0ull) ? 1 : 0;
     st_new += nc;
     tot += nc;  // the children occupy [old tot, old tot + nc)
     if (MZ_STAMPS && stl) {
@@ -658,6 +728,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     int cursor = 0, tot = 1;
     long long st_new = 0;
     int nc;
+    int wild = (g.N > 1) ? 1 : 0;  // joint-action trees always take the exact selection
     if (g.N > 1) {  // joint actions: the root's [N][A] inputs staged in (dynamic) LDS
         extern __shared__ __attribute__((aligned(16))) unsigned char jsm[];
         const int NA = g.NA;
@@ -679,7 +750,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         const float bet = (l < A) ? a.beta[ib + l] : 0.f;
         const float noi = (l < A) ? a.noise[ib + l] : 0.f;
         nc = expand_node(g, d, t, 0, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false, 0u,
-                         0u, nullptr);
+                         0u, nullptr, wild);
     }
     if (l == 0) {
         // root: CNode(1,1,1,1,true) (cnode.cpp:217), expanded, visit += 1, subtree.update(value, 0)
@@ -707,6 +778,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         h.mm_max = 0.f;
         h.mm_cnt = 0;
         h.leaf = 0;
+        h.tame = (!wild && tame_val(v) && tame_val(r)) ? 1 : 0;
         for (int j = 0; j < kNxt; ++j) h.nxt[j] = (cursor + j < kMtN) ? w0[cursor + j] : 0u;
         d.hdr()[t] = h;
         d.path()[(size_t)t * g.PS] = make_int2(0, 1);
@@ -715,6 +787,45 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         st[MZ_S_NEW_CHILDREN] += st_new;
         if (err) atomicOr(d.err(), err);
     }
+}
+
+// Bootstrap recurrence b = r + disc * b (cnode.cpp:448) over `n` levels, lane-parallel: level
+// i sits at lane 63 - (top - i), lane 63 holds the chunk's starting value (outside EXEC for the
+// whole loop), and each step every lane takes its upper neighbour's b through DPP wave_shl:1
+// fused into the multiply (tmp = b[l+1] * disc), then adds its own reward: after n steps lanes
+// 63-n .. 62 hold exactly the sequential recurrence's values.  The lane below the carry has tmp
+// preset to disc * carry, so it is right whether DPP reads an inactive source lane or leaves
+// the destination untouched.  Measured ~30 cycles per level, against ~46 for a wave-uniform
+// chain fed by v_readlane (each v_readlane costs ~30 cycles on gfx950).
+__device__ __forceinline__ void boot_dpp(float &b, float &tmp, float dv, float rn, int n) {
+    unsigned long long saved;
+    int n4 = n >> 2, n1 = n & 3;
+#define MZ_BOOT_STEP                                                                   \
+    "s_nop 1\n"                                                                        \
+    "v_mul_f32_dpp %[t], %[b], %[d] wave_shl:1 row_mask:0xf bank_mask:0xf\n"           \
+    "v_add_f32 %[b], %[r], %[t]\n"
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n"
+        "s_bitset0_b64 exec, 63\n"
+        "s_cmp_eq_u32 %[n4], 0\n"
+        "s_cbranch_scc1 2f\n"
+        "1:\n" MZ_BOOT_STEP MZ_BOOT_STEP MZ_BOOT_STEP MZ_BOOT_STEP
+        "s_sub_u32 %[n4], %[n4], 1\n"
+        "s_cmp_lg_u32 %[n4], 0\n"
+        "s_cbranch_scc1 1b\n"
+        "2:\n"
+        "s_cmp_eq_u32 %[n1], 0\n"
+        "s_cbranch_scc1 4f\n"
+        "3:\n" MZ_BOOT_STEP
+        "s_sub_u32 %[n1], %[n1], 1\n"
+        "s_cmp_lg_u32 %[n1], 0\n"
+        "s_cbranch_scc1 3b\n"
+        "4:\n"
+        "s_mov_b64 exec, %[sv]\n"
+        : [b] "+v"(b), [t] "+v"(tmp), [sv] "=&s"(saved), [n4] "+s"(n4), [n1] "+s"(n1)
+        : [d] "v"(dv), [r] "v"(rn)
+        : "memory", "scc");
+#undef MZ_BOOT_STEP
 }
 
 // --------------------------------------------------------------------------------------------
@@ -780,30 +891,42 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
     const int l = lane_id();
     const unsigned long long b0 = (MZ_STAMPS != 0) ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long b1 = 0, bw = 0;
+#ifdef MZ_PROBE5
+    unsigned long long pre5 = 0;
+#endif
     // bootstrap values (cnode.cpp:424,448): b_{i-1} = reward_i + discount * b_i from b_D = value,
-    // one f32 multiply and one add per level, in the reference's order.  Lane j holds level
-    // lo + j of a chunk of up to 64 levels; every step shifts the chunk down one lane with DPP
-    // (wave_shl:1: lane j receives lane j+1) and recomputes all lanes at once, so after
-    // (hi - lo) steps lane j holds exactly the sequential recurrence's b (each lane's last update
-    // uses its converged upper neighbour).  No cross-lane round trip per level.
+    // one f32 multiply and one add per level, in the reference's order, in chunks of up to 63
+    // levels (boot_dpp): lane j of a chunk topped by level hi holds level hi - 63 + j.
     {
         float carry = value;
         int hi = D;
+        const float dv = disc;
         while (true) {
             const int lo = hi > 63 ? hi - 63 : 0;
             const int nl = hi - lo;  // steps of this chunk
-            const int lev = lo + l;
+            const int lev = hi - 63 + l;
             float rn = 0.f;  // reward of the level above this lane's
-            if (lev < hi) rn = (lev + 1 == D) ? reward : i2f(s.A[s.path[lev + 1].x].w);
-            float b = (l == nl) ? carry : 0.f;
-            for (int k = 0; k < nl; ++k) {
-                const float up = i2f(__builtin_amdgcn_update_dpp(f2i(b), f2i(b), 0x130, 0xf, 0xf, false));
-                const float nb = rn + disc * up;
-                b = (l < nl) ? nb : b;
+            if (lev >= lo && lev < hi) {
+                const int up = (g.K == 1) ? lev + 1 : s.path[lev + 1].x;  // K = 1: path[i] = node i
+                rn = (lev + 1 == D) ? reward : i2f(s.A[up].w);
             }
-            if (l <= nl) s.boot[lev] = b;
+            float b = (l == 63) ? carry : 0.f;
+            float tmp = (l == 62) ? disc * carry : 0.f;
+#ifdef MZ_PROBE5  // diagnostic: everything outstanding drained before the chain itself
+            {
+                unsigned long long q;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(q)::"memory");
+                if (hi == D) pre5 = q;
+            }
+#endif
+            int steps = nl;
+#ifdef MZ_ABL_NOBOOT  // ablation (timing experiments only): no recurrence
+            steps = 0;
+#endif
+            boot_dpp(b, tmp, dv, rn, steps);
+            if (lev >= lo && lev <= hi) s.boot[lev] = b;
             if (lo == 0) break;
-            carry = rlf(b, 0);
+            carry = rlf(b, 63 - nl);  // level lo, the next chunk's top
             hi = lo;
         }
     }
@@ -937,6 +1060,9 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         wait_lds();
         const unsigned long long b2 = __builtin_amdgcn_s_memtime();
         stl[MZ_S_CYC_BAK_BOOT] += (long long)(b1 - b0);
+#ifdef MZ_PROBE5
+        stl[MZ_S_CYC_MINMAX] += (long long)(pre5 - b0);  // entry -> chain start (all drained)
+#endif
         stl[MZ_S_CYC_BAK_WAIT] += (long long)bw;
         stl[MZ_S_CYC_BAK_NODES] += (long long)(b2 - b1 - bw);
     }
@@ -1037,7 +1163,8 @@ __device__ __forceinline__ float path_score(const Geo &g, const Lds &s, int pare
 // its score checked in parallel afterwards; a failed check re-walks exactly.
 // --------------------------------------------------------------------------------------------
 __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base,
-                            unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl) {
+                            unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl,
+                            bool fast) {
     const int l = lane_id();
     const int cursor0 = h.cursor;
     const int wbase = cursor0;  // register window [wbase, wbase + 128)
@@ -1049,17 +1176,33 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
         int words = 0;
         if (!err) {
             const int root_visit = uni(s.A[0].x);
-            for (int base = 0; base <= D; base += kWave) {
-                const int i = base + l;
-                bool valid = false;
-                if (i <= D) {
-                    s.path[i] = make_int2(i, s.A[i].x);
-                    if (i >= 1 && !(i == 1 && root_visit <= 1)) {
-                        const float sc = path_score(g, s, i - 1, i, err);
-                        valid = sc >= -1000000.0f;  // tie list non-empty (FLOAT_MIN, utils.h:12)
-                    }
+            if (fast) {
+                // Every level's tie list is non-empty: the pUCT coefficients are finite and >= 0
+                // (fast_ok), priors lie in [0, 1e30] and rewards / values in [-1e30, 1e30]
+                // (TreeHdr::tame), so with |discount| <= 1, 0 <= lambda <= 1 and delta_lb > 0 every
+                // q, min/max bound and normalised value is finite, the value score lies in [0, 1]
+                // and the score prior_score + value_score is >= 0 (+inf at worst), never NaN.
+                // Each level consumes one word except the forced root child (cnode.cpp:398-399).
+                // Parent visit totals stay below the table size (root visits <= S + 1 < PS).
+                if (root_visit - 1 >= g.PS) err |= kErrTable;
+                words = D - ((root_visit <= 1) ? 1 : 0);
+                for (int base = 0; base <= D; base += kWave) {
+                    const int i = base + l;
+                    if (i <= D) s.path[i] = make_int2(i, s.A[i].x);
                 }
-                words += __popcll(ballot(valid));
+            } else {
+                for (int base = 0; base <= D; base += kWave) {
+                    const int i = base + l;
+                    bool valid = false;
+                    if (i <= D) {
+                        s.path[i] = make_int2(i, s.A[i].x);
+                        if (i >= 1 && !(i == 1 && root_visit <= 1)) {
+                            const float sc = path_score(g, s, i - 1, i, err);
+                            valid = sc >= -1000000.0f;  // tie list non-empty (FLOAT_MIN, utils.h:12)
+                        }
+                    }
+                    words += __popcll(ballot(valid));
+                }
             }
             scored = D;
         }
@@ -1230,16 +1373,32 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // (-mllvm -amdgpu-kernarg-preload-count) the first 16 dwords arrive in SGPRs at wave launch, so the
 // round-1 addresses do not wait for a kernel-argument load.
 template <bool EB, bool SEL, int NC, bool JOINT>
-__global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, const float *reward, const float *value,
-                                              const float *policy, const float *beta, int hsx, int ne, int pe, int K,
-                                              float discount, const char *pool, long long pool_stride,
+__global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, int A, int gK, int K, int ne,
+                                              int pe, const float *policy, const float *beta,
+                                              const Params *__restrict__ prm, const float *reward, const float *value,
+                                              int hsx, float discount, int fast_ok, const char *pool, long long pool_stride,
                                               long long row_bytes, char *gather_out, int *idx_x, int *idy, int *act) {
 #ifdef MZ_PROBE2
     unsigned long long pt0;
     asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(pt0)::"memory");
 #endif
-    const Geo g = prm->g;
-    const Dev d = prm->d;
+    // The geometry and the round-1 array offsets come from the preloaded arguments (the host
+    // passes exactly the Params block's values), so the first loads do not wait for Params.
+    // Compile-time layout classes read the rest of Params only after the round-1 loads are issued.
+    constexpr bool kLateParams = (NC > 0 && !JOINT);
+    Geo g;
+    Dev d;
+    if constexpr (!kLateParams) {
+        g = prm->g;
+        d = prm->d;
+    }
+    g.B = B;
+    g.P = P;
+    g.PS = PS;
+    g.A = A;
+    g.K = gK;
+    d.base = (gchar *)base;
+    arena_hot(d, B, P, PS);
     StepArgs a;
     a.reward = reward;
     a.value = value;
@@ -1277,21 +1436,6 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
     float *sJpol = JOINT ? (float *)(smem + g.oJpol) : nullptr;
     float *sJbet = JOINT ? (float *)(smem + g.oJbet) : nullptr;
     unsigned char *sJ = JOINT ? (smem + g.oJ) : nullptr;
-    if (EB) r_in = a.reward[t];
-    if (EB) v_in = a.value[t];
-    // gathered row chunks (four named registers: an array here ends up in scratch memory).  A K = 1
-    // tree is a chain: the next leaf is the child this simulation's expansion creates, whose
-    // parent has hidden_state_index_x = a.hsx, so its row is fetched now and checked after the
-    // selection.
-    bool gath_pending = false;
-    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
-    char *gdst = nullptr;
-    long long grb = 0;
-    const bool g_fast = SEL && a.pool &&
-                        (((a.row_bytes | a.pool_stride | (long long)(uintptr_t)a.pool |
-                           (long long)(uintptr_t)a.gather_out) & 15) == 0) &&
-                        a.row_bytes <= 4 * 16 * kWave;
-    const bool g_pre = EB && g_fast && g.K == 1;
 
 #ifdef MZ_PROBE
     unsigned long long pr0 = __builtin_amdgcn_s_memtime(), pr1 = 0, pr2 = 0;
@@ -1349,6 +1493,41 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
                 if (i0 + l < 2 * a.pe) glds4((const int *)(d.path() + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
         }
     }
+    // (the loads above take their addresses from preloaded arguments only; what needs the other
+    // kernel arguments or the Params block comes after them)
+    if constexpr (kLateParams) {
+        // no Params load (or its wait) above this point; the laundered address is typed constant
+        // memory again so the loads stay scalar
+        unsigned long long pv = (unsigned long long)(uintptr_t)prm;
+        asm volatile("" : "+s"(pv)::"memory");
+        const cParams *pl = (const cParams *)pv;
+        const Geo gl = pl->g;
+        const Dev dl = pl->d;
+        g = gl;
+        g.B = B;
+        g.P = P;
+        g.PS = PS;
+        g.A = A;
+        g.K = gK;
+        d = dl;
+        d.base = (gchar *)base;
+        arena_hot(d, B, P, PS);
+    }
+    if (EB) r_in = a.reward[t];
+    if (EB) v_in = a.value[t];
+    // gathered row chunks (four named registers: an array here ends up in scratch memory).  A K = 1
+    // tree is a chain: the next leaf is the child this simulation's expansion creates, whose
+    // parent has hidden_state_index_x = a.hsx, so its row is fetched now and checked after the
+    // selection.
+    bool gath_pending = false;
+    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+    char *gdst = nullptr;
+    long long grb = 0;
+    const bool g_fast = SEL && a.pool &&
+                        (((a.row_bytes | a.pool_stride | (long long)(uintptr_t)a.pool |
+                           (long long)(uintptr_t)a.gather_out) & 15) == 0) &&
+                        a.row_bytes <= 4 * 16 * kWave;
+    const bool g_pre = EB && g_fast && g.K == 1;
     long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
     // counters written per launch: the algorithmic ones, plus the cycle stamps in diagnostic builds
     constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
@@ -1361,6 +1540,7 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
         h.D = uni(hp->D);
         h.err = uni(hp->err);
         h.mm_cnt = uni(hp->mm_cnt);
+        h.tame = uni(hp->tame);
         h.mm_min = unif(hp->mm_min);
         h.mm_max = unif(hp->mm_max);
         h.leaf = uni(hp->leaf);
@@ -1382,6 +1562,12 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
         wait_vm();
     }
     stamp(ts, 1);
+#ifdef MZ_ABL_ROUND1  // ablation (timing experiments only): launch + round 1, nothing else
+    if (true) {
+        wait_vm();
+        return;
+    }
+#endif
     if (h.err) {  // a dead tree stays dead (both waves see the same header)
         if (SEL && wv == 0) {
             if (l == 0) {
@@ -1452,12 +1638,16 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
             const int leaf = h.leaf;
             long long st_new = 0;
             int nc;
-            if (JOINT)
+            if (JOINT) {
                 nc = expand_joint(g, d, t, leaf, sJpol, sJbet, nullptr, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, sJ,
                                   (double *)(smem + g.oJcp), (int *)(smem + g.oJdraw), err, st_new);
-            else
+                h.tame = 0;
+            } else {
+                int wild = 0;
                 nc = expand_node(g, d, t, leaf, pol, bet, 0.f, 0.f, a.K, v_in, cursor, ntot, s.rng, wbase, &s, err, st_new,
-                                 have_w, w1r, w2r, stl);
+                                 have_w, w1r, w2r, stl, wild);
+                if (wild || !tame_val(v_in) || !tame_val(r_in)) h.tame = 0;
+            }
             stl[MZ_S_EXPANDS] += 1;
             stl[MZ_S_NEW_CHILDREN] += st_new;
             if (!err && l == 0) {
@@ -1473,7 +1663,9 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
         } else {
             // ---- CTree::back_propagate (cnode.cpp:415-450) + the min/max normaliser ----
             stamp(ts, 4);
+#ifndef MZ_ABL_W1SKIP  // ablation (timing experiments only): no back-propagation
             backup(g, d, s, t, h.D, tot, v_in, r_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl);
+#endif
             stamp(ts, 5);
 #if defined(MZ_PROBE2) || defined(MZ_PROBE3)
             if (false) {
@@ -1527,16 +1719,19 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
 #ifdef MZ_PROBE3
         const unsigned long long v0 = __builtin_amdgcn_s_memtime();
 #endif
-        value_scores(g, s, h.tot, a.discount, h);
+        // K = 1 chains of a tame tree (TreeHdr::tame) under tame handle constants select without
+        // scoring: no score can be NaN or below FLOAT_MIN there (select_walk)
+        const bool fast = !JOINT && g.K == 1 && fast_ok && h.tame && fabsf(a.discount) <= 1.0f;
+        if (!fast) value_scores(g, s, h.tot, a.discount, h);
 #ifdef MZ_PROBE3
         stl[MZ_S_CYC_EXP_CDF] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // value scores
 #endif
         // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
         int perr = 0;  // words past the stream end only matter if the walk consumes them
-        const unsigned rw0 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
-        const unsigned rw1 = rng_word_lane(g, d, s.rng, wbase, t, h.cursor + kWave + l, perr);
+        const unsigned rw0 = fast ? 0u : rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
+        const unsigned rw1 = fast ? 0u : rng_word_lane(g, d, s.rng, wbase, t, h.cursor + kWave + l, perr);
         int idx = 0, act = 0;
-        select_walk(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl);
+        select_walk(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast);
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;
@@ -1595,6 +1790,7 @@ __global__ __launch_bounds__(128) void k_step(const Params *__restrict__ prm, co
             hp->mm_min = h.mm_min;
             hp->mm_max = h.mm_max;
             hp->mm_cnt = h.mm_cnt;
+            hp->tame = h.tame;
             hp->leaf = h.leaf;
         }
     }
@@ -1754,6 +1950,8 @@ struct mz_batch {
     bool rb_dev_valid = false;  // rb_dev mirrors the current tree state
     float rb_disc = 0.f;
     float tbl_c2 = NAN, tbl_c1 = NAN;
+    int consts_ok = 0;  // delta_lb > 0 and 0 <= lambda <= 1 (mz_create)
+    int fast_ok = 0;    // consts_ok and every pUCT coefficient finite and >= 0 (ensure_tables)
     bool prepared = false;
     long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
     int nc = 0;                // k_step layout class (0 = layout from Geo)
@@ -1831,6 +2029,9 @@ int ensure_tables(mz_batch *b, float c2, float c1) {
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->tbl_c2 = c2;
     b->tbl_c1 = c1;
+    bool pb_ok = true;
+    for (int n = 0; n < b->PS; ++n) pb_ok = pb_ok && std::isfinite(pb[n]) && pb[n] >= 0.f;
+    b->fast_ok = (b->consts_ok && pb_ok) ? 1 : 0;
     return MZ_OK;
 }
 
@@ -1872,9 +2073,9 @@ struct ArenaPlan {
 template <int NC, bool JOINT = false>
 void launch_nc(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
     const Geo &g = b->geo;
-#define MZ_STEP_ARGS                                                                                          \
-    b->prm, a.reward, a.value, a.policy, a.beta, a.hsx, a.ne, a.pe, a.K, a.discount, a.pool, a.pool_stride, \
-        a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act
+#define MZ_STEP_ARGS                                                                                       \
+    (char *)b->dev.base, g.B, g.P, g.PS, g.A, g.K, a.K, a.ne, a.pe, a.policy, a.beta, b->prm, a.reward, a.value,     \
+        a.hsx, a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act
     if (eb && sel)
         hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, MZ_STEP_ARGS);
     else if (eb)
@@ -2017,6 +2218,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.seed = seed;
     g.one_minus_rho = 1 - rho;
     g.delta = delta_lb;
+    b->consts_ok = (delta_lb > 0.f && std::isfinite(delta_lb) && lam >= 0.f && lam <= 1.f) ? 1 : 0;
     {
         // worst case of sum(visits) over a path: every value entry of the tree
         const long long worst = 1ll + S + (long long)S * (S + 1) / 2;
@@ -2043,7 +2245,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oSq = o; o += round16(8 * (g.PS + kWave));
     g.oLp = o; o += round16(4 * (g.PS + 1 + kWave));
     g.oRng = o; o += round16(4 * kRngWin);
-    g.oBoot = o; o += round16(4 * g.PS);
+    g.oBoot = o; o += round16(4 * (g.PS + kWave));
     g.oReg = o; o += round16(8 * g.reg_cap);
     g.oX = o; o += round16(8 * (2 * MZ_S_COUNT + 2));
     g.oPar = o; o += round16(4 * g.P);
@@ -2121,6 +2323,16 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         plan.ptr(&b->rb_dev, b->rb_words);
         plan.dev<int2>(d.o_V, nodes * b->E);
         rc = plan.allocate(b, d);
+        if (!rc) {
+            Dev chk = d;
+            arena_hot(chk, B, b->P, b->PS);
+            const bool same = chk.o_hdr == d.o_hdr && chk.o_stats == d.o_stats && chk.o_err == d.o_err &&
+                              chk.o_seed == d.o_seed && chk.o_lp == d.o_lp && chk.o_T == d.o_T && chk.o_pb == d.o_pb &&
+                              chk.o_sq == d.o_sq && chk.o_A == d.o_A && chk.o_Par == d.o_Par && chk.o_Bn == d.o_Bn &&
+                              chk.o_Q == d.o_Q && chk.o_PP == d.o_PP && chk.o_C == d.o_C && chk.o_path == d.o_path;
+            if (!same || (char *)b->prm != (char *)d.base)
+                rc = fail(MZ_ERR_RUNTIME, "internal: arena layout differs from arena_hot()");
+        }
     }
     if (rc) {
         std::string m = g_err;
