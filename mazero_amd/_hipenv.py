@@ -1,23 +1,35 @@
 """HIP runtime settings this package depends on, applied at import, before the runtime initialises.
 
-DEBUG_CLR_GRAPH_PACKET_CAPTURE=0: with the runtime's default graph "packet capture", a captured
-search graph replayed after a few thousand ordinary kernel launches on the same device (eager
-searches between two replays, for example) ran with corrupted arguments in some of its kernels:
-the searches reported errors (or could differ) although the same graph replayed correctly before
-and after.  Disabling packet capture makes every replay marshal its kernel arguments afresh
-(tests/test_driver.py::test_graph_replay_after_eager_launches); it costs about 1% of the fused
-kernel's per-launch time (6.69 -> 6.78 us, 3m K=1).
+History.  Earlier in round 1 a captured search graph replayed after a few thousand ordinary kernel
+launches ran with corrupted arguments in some of its kernels (tests/test_driver.py::
+test_graph_replay_after_eager_launches), and the package then set
+DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 so that every replay marshalled its arguments afresh.  That
+setting doubles the cost of every kernel launch in a graph (measured with scripts/launch.hip: an
+empty kernel with k_step's 20 arguments costs 1.72 us per launch with packet capture, 3.75 us
+without), which was half of the fused tree kernel's 6.4 us per simulation.
 
-The runtime reads the variable once, when it initialises.  If the process initialised HIP before
-importing mazero_amd without setting it, search graphs are not safe to replay and SampledMCTS runs
-its loop eagerly instead (GRAPHS_SAFE is False).
+With the current argument layout (14 dwords preloaded into SGPRs by the command processor, the
+rest read once from a device Params block) the regression test and a 40-replay stress
+(scripts/debug_graph_stress.py, ~8,000 eager launches between replays) pass with packet capture
+on, with and without the settings below.  The symptom ("some launches saw wrong arguments") is
+that of kernel arguments read stale through the host-data-path write combiner, so the package
+keeps the runtime's kernarg HDP-flush workaround on:
+
+    DEBUG_CLR_KERNARG_HDP_FLUSH_WA=1   (no measurable launch cost)
+
+and leaves packet capture at the runtime default.  A user who sets
+DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 keeps the old, slower behaviour.
+
+The runtime reads these variables once, when it initialises.  If the process initialised HIP
+before importing mazero_amd without them, SampledMCTS runs its loop eagerly (GRAPHS_SAFE False).
 """
 from __future__ import annotations
 
 import os
 import sys
 
-KEY = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+KEY = "DEBUG_CLR_KERNARG_HDP_FLUSH_WA"
+KEY_CAPTURE = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
 
 
 def _hip_initialised() -> bool:
@@ -31,6 +43,9 @@ def _hip_initialised() -> bool:
 
 
 _user = os.environ.get(KEY)
+_user_capture = os.environ.get(KEY_CAPTURE)
 _late = _hip_initialised()
-os.environ.setdefault(KEY, "0")
-GRAPHS_SAFE = (_user == "0") or (_user is None and not _late)
+os.environ.setdefault(KEY, "1")
+GRAPHS_SAFE = (_user == "1") or (_user_capture == "0") or (_user is None and not _late)
+if os.environ.get("MZ_GRAPH_ENV_EXPERIMENT") == "1":  # diagnostics: other runtime settings under test
+    GRAPHS_SAFE = True

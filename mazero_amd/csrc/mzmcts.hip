@@ -185,8 +185,10 @@ __host__ __device__ __forceinline__ void arena_hot(Dev &d, long long B, long lon
 
 #ifdef __HIP_DEVICE_COMPILE__
 typedef const __attribute__((address_space(4))) Params cParams;
+typedef const __attribute__((address_space(4))) TreeHdr cTreeHdr;
 #else
 typedef const Params cParams;
+typedef const TreeHdr cTreeHdr;
 #endif
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) void glb_void;
@@ -219,6 +221,10 @@ __device__ __forceinline__ int pack_y(int nc, int act, int md) { return nc | (ac
 // Wait for this wave's memory traffic (LDS-DMA included via vmcnt) / LDS traffic; compiler fence.
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Workgroup barrier for data exchanged through LDS only: unlike __syncthreads() it does not wait for
+// the wave's outstanding global stores (vmcnt), which take ~1,000 cycles to drain.  LDS-DMA data
+// a wave hands over must be waited for (wait_vm) before it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n s_barrier" ::: "memory"); }
 
 // LDS-DMA: lane l copies `bytes` (4 or 16) from its own src into lds_base + l*bytes (lds_base
 // must be wave-uniform).
@@ -255,6 +261,26 @@ __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, i2f(dpp<0x141>(f2i(v))));
     v = fmaxf(v, i2f(dpp<0x140>(f2i(v))));
     return fmaxf(fmaxf(rlf(v, 0), rlf(v, 16)), fmaxf(rlf(v, 32), rlf(v, 48)));
+}
+// Full-wave min / max whose result is exact in lane 63 only: the row reduction of wave_min, then
+// row_bcast:15 / row_bcast:31 fold rows 0-1 and 2-3 into lane 63 (no v_readlane).
+__device__ __forceinline__ float wave_min_to63(float v) {
+    v = fminf(v, i2f(dpp<0xB1>(f2i(v))));
+    v = fminf(v, i2f(dpp<0x4E>(f2i(v))));
+    v = fminf(v, i2f(dpp<0x141>(f2i(v))));
+    v = fminf(v, i2f(dpp<0x140>(f2i(v))));
+    v = fminf(v, i2f(__builtin_amdgcn_update_dpp(f2i(v), f2i(v), 0x142, 0xa, 0xf, false)));  // row_bcast:15
+    v = fminf(v, i2f(__builtin_amdgcn_update_dpp(f2i(v), f2i(v), 0x143, 0xc, 0xf, false)));  // row_bcast:31
+    return v;
+}
+__device__ __forceinline__ float wave_max_to63(float v) {
+    v = fmaxf(v, i2f(dpp<0xB1>(f2i(v))));
+    v = fmaxf(v, i2f(dpp<0x4E>(f2i(v))));
+    v = fmaxf(v, i2f(dpp<0x141>(f2i(v))));
+    v = fmaxf(v, i2f(dpp<0x140>(f2i(v))));
+    v = fmaxf(v, i2f(__builtin_amdgcn_update_dpp(f2i(v), f2i(v), 0x142, 0xa, 0xf, false)));
+    v = fmaxf(v, i2f(__builtin_amdgcn_update_dpp(f2i(v), f2i(v), 0x143, 0xc, 0xf, false)));
+    return v;
 }
 __device__ __forceinline__ int wave_sum(int v) {
     v += dpp<0xB1>(v);
@@ -317,7 +343,7 @@ struct Layout {
     static constexpr int oBoot = oRng + r16(4 * kRngWin);
     static constexpr int oReg = oBoot + r16(4 * (NC + kWave));
     static constexpr int oX = oReg + r16(8 * kRegCap);
-    static constexpr int oPar = oX + r16(8 * (2 * MZ_S_COUNT + 2));
+    static constexpr int oPar = oX + r16(8 * (2 * MZ_S_COUNT + 4));
     static constexpr int oSc = oPar + r16(4 * NC);
     static constexpr int total = oSc + r16(4 * NC);
 };
@@ -496,6 +522,9 @@ __device__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float 
         e2 = __builtin_amdgcn_s_memtime();
         if (e1 == 0) e1 = e0;
     }
+    // the loads still in flight (the RNG window, the leaf's record, a prefetched row) land before
+    // this expansion's stores are issued, so later waits need not drain the stores
+    wait_vm();
     const bool has = (l < A) && cnt > 0;
     const unsigned long long m = ballot(has);
     const int nc = __popcll(m);
@@ -844,10 +873,17 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
     need = 0;
     off = 0;
     if (i <= D) {
-        const int2 pe = s.path[i];
-        n = pe.x;
-        nv = pe.y;
-        need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
+        if (g.K == 1) {
+            // K = 1 trees are chains: the path is node i at level i, its entry count the visit
+            // count staged this launch, and every update appends with an empty depth class
+            n = i;
+            nv = s.A[i].x;
+        } else {
+            const int2 pe = s.path[i];
+            n = pe.x;
+            nv = pe.y;
+            need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
+        }
     }
     const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
     // prefix sum of the needed entry counts over the chunk: a uniform loop over the needing lanes
@@ -887,7 +923,8 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
 // multiset's content.  Chunk 0's entries must already be in flight (stage_regions).
 // --------------------------------------------------------------------------------------------
 __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float reward, float disc,
-                       TreeHdr &h, int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl) {
+                       TreeHdr &h, int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl,
+                       float *xmm) {
     const int l = lane_id();
     const unsigned long long b0 = (MZ_STAMPS != 0) ? __builtin_amdgcn_s_memtime() : 0ull;
     unsigned long long b1 = 0, bw = 0;
@@ -1044,11 +1081,12 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
         for (unsigned long long m = ballot(l < cnt && nv > pos); m; m &= m - 1ull) {
             const int j = __builtin_ctzll(m);
             const int nvj = rl(nv, j), posj = rl(pos, j), offj = rl(off, j), nj = rl(n, j);
+            ent_w += nvj - posj;
             int2 *Gj = gV + (size_t)nj * g.E;
             for (int e0 = posj; e0 < nvj; e0 += kWave)
                 if (e0 + l < nvj) Gj[e0 + l + 1] = s.reg[offj + e0 + l];
         }
-        ent_w += wave_sum((l < cnt) ? (nv - pos + 1) : 0);
+        ent_w += cnt;  // each updated node writes its new entry (plus the tail shifts above)
         wait_lds();
         i0 += cnt;
         if (i0 <= D) cnt = stage_regions(g, d, s, t, D, i0, n, nv, need, off);
@@ -1068,20 +1106,27 @@ __device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot
     }
     // min/max over the q of visited non-root nodes (`tot` = the node count before this
     // simulation's expansion: the new children are unvisited, and the other wave writes them)
+    // The reductions end in lane 63 (no v_readlane, ~30 cycles each on gfx950), which hands
+    // min / max to the other wave through LDS; the count is a scalar popcount of ballots.
     float mn = INFINITY, mx = -INFINITY;
     int cv = 0;
     for (int base = 1; base < tot; base += kWave) {
         const int nn = base + l;
-        if (nn < tot && s.A[nn].x > 0) {
+        const bool on = nn < tot && s.A[nn].x > 0;
+        if (on) {
             const float q = s.Q[nn];
             mn = fminf(mn, q);
             mx = fmaxf(mx, q);
-            ++cv;
         }
+        cv += __popcll(ballot(on));
     }
-    h.mm_min = wave_min(mn);
-    h.mm_max = wave_max(mx);
-    h.mm_cnt = wave_sum(cv);
+    mn = wave_min_to63(mn);
+    mx = wave_max_to63(mx);
+    if (l == 63) {
+        xmm[0] = mn;
+        xmm[1] = mx;
+    }
+    h.mm_cnt = cv;
     stl[MZ_S_MINMAX_NODES] += tot - 1;
 }
 
@@ -1186,16 +1231,11 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
                 // Parent visit totals stay below the table size (root visits <= S + 1 < PS).
                 if (root_visit - 1 >= g.PS) err |= kErrTable;
                 words = D - ((root_visit <= 1) ? 1 : 0);
-                for (int base = 0; base <= D; base += kWave) {
-                    const int i = base + l;
-                    if (i <= D) s.path[i] = make_int2(i, s.A[i].x);
-                }
             } else {
                 for (int base = 0; base <= D; base += kWave) {
                     const int i = base + l;
                     bool valid = false;
                     if (i <= D) {
-                        s.path[i] = make_int2(i, s.A[i].x);
                         if (i >= 1 && !(i == 1 && root_visit <= 1)) {
                             const float sc = path_score(g, s, i - 1, i, err);
                             valid = sc >= -1000000.0f;  // tie list non-empty (FLOAT_MIN, utils.h:12)
@@ -1216,9 +1256,7 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
         stl[MZ_S_SELECTS] += 1;
         stl[MZ_S_PATH_EDGES] += D;
         stl[MZ_S_SCORED] += scored;
-        wait_lds();
-        int2 *gp = d.path() + (size_t)t * g.PS;
-        for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
+        // (no path record: the next back-propagation walks the chain itself, stage_regions)
         return;
     }
 
@@ -1373,21 +1411,30 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 // (-mllvm -amdgpu-kernarg-preload-count) the first 16 dwords arrive in SGPRs at wave launch, so the
 // round-1 addresses do not wait for a kernel-argument load.
 template <bool EB, bool SEL, int NC, bool JOINT>
-__global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, int A, int gK, int K, int ne,
-                                              int pe, const float *policy, const float *beta,
-                                              const Params *__restrict__ prm, const float *reward, const float *value,
-                                              int hsx, float discount, int fast_ok, const char *pool, long long pool_stride,
-                                              long long row_bytes, char *gather_out, int *idx_x, int *idy, int *act) {
+__global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA, int pk, const float *reward,
+                                              const float *value, const float *policy, const float *beta, int K,
+                                              int hsx, float discount,
+                                              int fast_ok, const char *pool, long long pool_stride, long long row_bytes,
+                                              char *gather_out, int *idx_x, int *idy, int *act) {
 #ifdef MZ_PROBE2
     unsigned long long pt0;
     asm volatile("s_memtime %0\n s_waitcnt lgkmcnt(0)" : "=s"(pt0)::"memory");
 #endif
-    // The geometry and the round-1 array offsets come from the preloaded arguments (the host
-    // passes exactly the Params block's values), so the first loads do not wait for Params.
-    // Compile-time layout classes read the rest of Params only after the round-1 loads are issued.
+#ifdef MZ_ABL_EMPTY  // ablation (timing experiments only): launch cost of this kernel
+    if (true) return;
+#endif
+    // The first 14 argument dwords arrive in SGPRs (kernel-argument preloading): the arena base,
+    // the geometry (B | A << 24, path bound | handle K << 17: the host passes exactly the Params
+    // block's values) and the four network-output pointers, so every round-1 address is computed
+    // without a memory round trip.  Compile-time layout classes read the other arguments and the
+    // rest of Params in one batch after the round-1 loads are issued (kLateParams).
     constexpr bool kLateParams = (NC > 0 && !JOINT);
+    const int B = BA & 0xffffff, A = (int)((unsigned)BA >> 24);
+    const int pe = pk & 0x1ffff, gK = (int)((unsigned)pk >> 17);
+    const int ne = (1ll + (long long)gK * (pe - 1)) < P ? 1 + gK * (pe - 1) : P;  // node bound (launch_step)
     Geo g;
     Dev d;
+    const Params *prm = (const Params *)base;  // the Params block heads the arena (mz_create)
     if constexpr (!kLateParams) {
         g = prm->g;
         d = prm->d;
@@ -1432,7 +1479,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
     // ---- round 1: everything that does not depend on the tree header, issued with it --------
     float pol = 0.f, bet = 0.f, r_in = 0.f, v_in = 0.f;
     unsigned w1r = 0u, w2r = 0u;
-    const bool have_w = !JOINT && 2 * a.K <= kNxt;
+    const bool have_w = !JOINT && 2 * g.K <= kNxt;  // (call K <= handle K)
     float *sJpol = JOINT ? (float *)(smem + g.oJpol) : nullptr;
     float *sJbet = JOINT ? (float *)(smem + g.oJbet) : nullptr;
     unsigned char *sJ = JOINT ? (smem + g.oJ) : nullptr;
@@ -1468,7 +1515,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
                 pol = a.policy[ib + l];
                 bet = a.beta[ib + l];
             }
-            if (have_w && l < a.K) {
+            if (have_w && l < g.K) {
                 w1r = d.hdr()[t].nxt[2 * l];
                 w2r = d.hdr()[t].nxt[2 * l + 1];
             }
@@ -1489,32 +1536,70 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
         if (EB) {
             for (int i0 = 0; i0 < g.PS + 1; i0 += kWave)
                 if (i0 + l < g.PS + 1) glds4(d.lp() + i0 + l, s.lp + i0);
-            for (int i0 = 0; i0 < 2 * a.pe; i0 += kWave)
-                if (i0 + l < 2 * a.pe) glds4((const int *)(d.path() + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
+            if (g.K > 1)  // (K = 1 chains need no path: stage_regions)
+                for (int i0 = 0; i0 < 2 * a.pe; i0 += kWave)
+                    if (i0 + l < 2 * a.pe)
+                        glds4((const int *)(d.path() + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
         }
     }
     // (the loads above take their addresses from preloaded arguments only; what needs the other
     // kernel arguments or the Params block comes after them)
-    if constexpr (kLateParams) {
-        // no Params load (or its wait) above this point; the laundered address is typed constant
-        // memory again so the loads stay scalar
-        unsigned long long pv = (unsigned long long)(uintptr_t)prm;
-        asm volatile("" : "+s"(pv)::"memory");
-        const cParams *pl = (const cParams *)pv;
-        const Geo gl = pl->g;
-        const Dev dl = pl->d;
-        g = gl;
-        g.B = B;
-        g.P = P;
-        g.PS = PS;
-        g.A = A;
-        g.K = gK;
-        d = dl;
-        d.base = (gchar *)base;
-        arena_hot(d, B, P, PS);
+    TreeHdr h;
+    {
+        // scalar loads straight into SGPRs (no v_readfirstlane, ~30 cycles each on gfx950): the
+        // header was written by an earlier launch and the scalar cache starts every dispatch
+        // invalidated; this launch writes it only after reading it
+        const cTreeHdr *hp = (const cTreeHdr *)(d.hdr() + t);
+        h.cursor = hp->cursor;
+        h.tot = hp->tot;
+        h.D = hp->D;
+        h.err = hp->err;
+        h.mm_cnt = hp->mm_cnt;
+        h.tame = hp->tame;
+        h.mm_min = hp->mm_min;
+        h.mm_max = hp->mm_max;
+        h.leaf = hp->leaf;
     }
-    if (EB) r_in = a.reward[t];
-    if (EB) v_in = a.value[t];
+    if (EB) {  // this simulation's network outputs for the leaf (both waves)
+        r_in = reward[t];
+        v_in = value[t];
+    }
+#ifdef MZ_ABL_VEC1  // ablation (timing experiments only): launch + the preloaded-address loads only
+    if (true) {
+        wait_vm();
+        return;
+    }
+#endif
+    if constexpr (kLateParams) {
+        // Params heads the arena: scalar loads from the preloaded base (the scheduler may issue
+        // them earlier; nothing above waits for them)
+        const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
+        g.K = pl->g.K;  // (equals gK)
+        g.S = pl->g.S;
+        g.E = pl->g.E;
+        g.W = pl->g.W;
+        g.TT = pl->g.TT;
+        g.use_table = 0;  // compile-time layout classes compute pUCT coefficients from pb / sq
+        g.root_offset = pl->g.root_offset;
+        g.seed = pl->g.seed;
+        g.one_minus_rho = pl->g.one_minus_rho;
+        g.delta = pl->g.delta;
+        g.reg_cap = pl->g.reg_cap;
+        g.N = 1;
+        g.NA = A;
+        g.JP = 0;
+        d.o_J = 0;
+        d.o_D = pl->d.o_D;
+        d.o_V = pl->d.o_V;
+        d.o_R = pl->d.o_R;
+        // every scalar the rest of the kernel reads, loaded here in one batch (one wait, while the
+        // round-1 vector loads are in flight) instead of lazily behind later branches
+        asm volatile("" ::"s"(g.K), "s"(g.E), "s"(g.W), "s"(g.one_minus_rho), "s"(g.delta), "s"(g.reg_cap),
+                     "s"(d.o_V), "s"(d.o_R), "s"(d.o_D), "s"(K), "s"(hsx), "s"(discount), "s"(fast_ok), "s"(pool),
+                     "s"(pool_stride), "s"(row_bytes), "s"(gather_out), "s"(idx_x), "s"(idy), "s"(act));
+        asm volatile("" ::"s"(h.cursor), "s"(h.tot), "s"(h.D), "s"(h.err), "s"(h.mm_cnt), "s"(h.tame), "s"(h.mm_min),
+                     "s"(h.mm_max), "s"(h.leaf));
+    }
     // gathered row chunks (four named registers: an array here ends up in scratch memory).  A K = 1
     // tree is a chain: the next leaf is the child this simulation's expansion creates, whose
     // parent has hidden_state_index_x = a.hsx, so its row is fetched now and checked after the
@@ -1532,19 +1617,6 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
     // counters written per launch: the algorithmic ones, plus the cycle stamps in diagnostic builds
     constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
     const long long st_old = (wv == 0 && l < kStatN) ? st[l] : 0;
-    TreeHdr h;
-    {
-        const TreeHdr *hp = d.hdr() + t;
-        h.cursor = uni(hp->cursor);
-        h.tot = uni(hp->tot);
-        h.D = uni(hp->D);
-        h.err = uni(hp->err);
-        h.mm_cnt = uni(hp->mm_cnt);
-        h.tame = uni(hp->tame);
-        h.mm_min = unif(hp->mm_min);
-        h.mm_max = unif(hp->mm_max);
-        h.leaf = uni(hp->leaf);
-    }
 #ifdef MZ_PROBE
     pr2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1599,7 +1671,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
                 }
             }
         }
-        if (EB)
+        if (EB && g.K > 1)
             for (int i0 = 2 * a.pe; i0 < 2 * (h.D + 1); i0 += kWave)
                 if (i0 + l < 2 * (h.D + 1))
                     glds4((const int *)(d.path() + (size_t)t * g.PS) + i0 + l, (int *)s.path + i0);
@@ -1664,7 +1736,8 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
             // ---- CTree::back_propagate (cnode.cpp:415-450) + the min/max normaliser ----
             stamp(ts, 4);
 #ifndef MZ_ABL_W1SKIP  // ablation (timing experiments only): no back-propagation
-            backup(g, d, s, t, h.D, tot, v_in, r_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl);
+            backup(g, d, s, t, h.D, tot, v_in, r_in, a.discount, h, cnt0, n0, nv0, need0, off0, err, stl,
+                   (float *)(xst + 2 * MZ_S_COUNT));
 #endif
             stamp(ts, 5);
 #if defined(MZ_PROBE2) || defined(MZ_PROBE3)
@@ -1682,14 +1755,14 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
                 for (int k = 0; k < kStatN; ++k) xst[MZ_S_COUNT + k] = stl[k];  // wave 1's counters
                 float *xf = (float *)(xst + 2 * MZ_S_COUNT);
                 int *xi = (int *)(xst + 2 * MZ_S_COUNT);
-                xf[0] = h.mm_min;
-                xf[1] = h.mm_max;
+                if (MZ_STAMPS) xst[2 * MZ_S_COUNT + 2] = (long long)ts[0];  // wave 1's start
+                (void)xf;  // min / max: written by lane 63 in backup()
                 xi[2] = h.mm_cnt;
                 xi[3] = err;
             }
         }
         if (JOINT && wv == 1) wait_vm();  // the joint actions staged for the selection
-        __syncthreads();
+        lds_barrier();  // the waves' global stores stay in flight
         if (wv == 1) {
             wait_vm();  // nothing of wave 1 may be in flight when the block ends
             return;
@@ -1698,6 +1771,8 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
         {
             const float *xf = (const float *)(xst + 2 * MZ_S_COUNT);
             const int *xi = (const int *)(xst + 2 * MZ_S_COUNT);
+            // diagnostic builds: how much later than wave 0 wave 1 started (in the 'minmax' slot)
+            if (MZ_STAMPS && SEL) stl[MZ_S_CYC_MINMAX] += xst[2 * MZ_S_COUNT + 2] - (long long)ts[0];
             h.mm_min = unif(xf[0]);
             h.mm_max = unif(xf[1]);
             h.mm_cnt = uni(xi[2]);
@@ -1713,7 +1788,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int B, int P, int PS, 
         if (wv == 1) return;
     }
     stamp(ts, 5);
-    wait_vm();  // RNG window (and anything staged) has landed
+    if (!EB || JOINT) wait_vm();  // RNG window (and anything staged) has landed (expand_node waited)
     stamp(ts, 6);
     if (SEL && !err) {
 #ifdef MZ_PROBE3
@@ -2074,8 +2149,9 @@ template <int NC, bool JOINT = false>
 void launch_nc(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
     const Geo &g = b->geo;
 #define MZ_STEP_ARGS                                                                                       \
-    (char *)b->dev.base, g.B, g.P, g.PS, g.A, g.K, a.K, a.ne, a.pe, a.policy, a.beta, b->prm, a.reward, a.value,     \
-        a.hsx, a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act
+    (char *)b->dev.base, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value, a.policy, a.beta,  \
+        a.K, a.hsx, a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy,      \
+        a.act
     if (eb && sel)
         hipLaunchKernelGGL((k_step<true, true, NC, JOINT>), dim3(g.B), dim3(2 * kWave), g.lds, b->stream, MZ_STEP_ARGS);
     else if (eb)
@@ -2172,6 +2248,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     if (!out) return fail(MZ_ERR_ARG, "null output handle");
     *out = nullptr;
     if (B < 1 || A < 1 || K < 1 || S < 0) return fail(MZ_ERR_ARG, "bad tree-batch dimensions");
+    if (B >= (1 << 24)) return fail(MZ_ERR_UNSUPPORTED, "root_num >= 2^24");  // packed with A in k_step's arguments
     if (N < 1) return fail(MZ_ERR_ARG, "agent_num must be >= 1");
     if (A > kMaxActions) return fail(MZ_ERR_UNSUPPORTED, "action_space_size > 64");
     if (N > 1 && (K > kWave || N > kWave || (long long)N * A > 4096))
@@ -2247,7 +2324,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oRng = o; o += round16(4 * kRngWin);
     g.oBoot = o; o += round16(4 * (g.PS + kWave));
     g.oReg = o; o += round16(8 * g.reg_cap);
-    g.oX = o; o += round16(8 * (2 * MZ_S_COUNT + 2));
+    g.oX = o; o += round16(8 * (2 * MZ_S_COUNT + 4));
     g.oPar = o; o += round16(4 * g.P);
     g.oSc = o; o += round16(4 * g.P);
     g.N = N;

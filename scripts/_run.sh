@@ -1,1 +1,1 @@
-bash scripts/iter.sh && K=1 VARIANTS="abl_NOBOOT abl_W1SKIP" bash scripts/ablate.sh
+bash scripts/iter.sh && K=1 VARIANTS="abl_W1SKIP" bash scripts/ablate.sh

@@ -325,9 +325,8 @@ def test_driver_graph_replay_matches_oracle(K, port_lib):
 @pytest.mark.gpu
 def test_graph_replay_after_eager_launches(port_lib):
     """A captured search graph replayed after thousands of ordinary launches (eager searches of the
-    same configuration) still matches the oracle.  With the HIP runtime's graph packet capture on
-    (DEBUG_CLR_GRAPH_PACKET_CAPTURE unset or 1) this exact sequence failed in agent 1's replay:
-    mazero_amd/_hipenv.py."""
+    same configuration) still matches the oracle.  Earlier in round 1 this exact sequence failed
+    in agent 1's replay under the runtime's graph packet capture (mazero_amd/_hipenv.py)."""
     import torch
 
     from consume import eps_greedy_given, select_action
