@@ -1,35 +1,29 @@
 """HIP runtime settings this package depends on, applied at import, before the runtime initialises.
 
-History.  Earlier in round 1 a captured search graph replayed after a few thousand ordinary kernel
-launches ran with corrupted arguments in some of its kernels (tests/test_driver.py::
-test_graph_replay_after_eager_launches), and the package then set
-DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 so that every replay marshalled its arguments afresh.  That
-setting doubles the cost of every kernel launch in a graph (measured with scripts/launch.hip: an
-empty kernel with k_step's 20 arguments costs 1.72 us per launch with packet capture, 3.75 us
-without), which was half of the fused tree kernel's 6.4 us per simulation.
+DEBUG_CLR_GRAPH_PACKET_CAPTURE=0.  With the runtime's default graph "packet capture", a captured
+search graph replayed after a few thousand ordinary kernel launches ran with corrupted arguments
+in some of its kernels: agent 1's search of tests/test_driver.py::
+test_graph_replay_after_eager_launches reports "search path or value-set capacity exceeded",
+reproducibly, while the same sequence without the eager searches between capture and replay, or
+with packet capture off, matches the oracle (scripts/debug_driver_graph.py).  It does not depend
+on kernel-argument preloading, and the runtime's kernarg HDP-flush workaround
+(DEBUG_CLR_KERNARG_HDP_FLUSH_WA=1) does not cure it: an earlier commit relied on that workaround
+and the regression test failed again on the next fresh box.  A plain torch graph under similar
+churn (scripts/debug_torch_graph.py) replays correctly, so the trigger is specific to this launch
+mix; turning packet capture off is the fix that holds.  Every replay then marshals its kernel
+arguments afresh; on the 3m K=1 bench that costs 0.4 % of the fused kernel's time (5.566 ->
+5.588 us per launch, 1 x MI355X).
 
-With the current argument layout (14 dwords preloaded into SGPRs by the command processor, the
-rest read once from a device Params block) the regression test and a 40-replay stress
-(scripts/debug_graph_stress.py, ~8,000 eager launches between replays) pass with packet capture
-on, with and without the settings below.  The symptom ("some launches saw wrong arguments") is
-that of kernel arguments read stale through the host-data-path write combiner, so the package
-keeps the runtime's kernarg HDP-flush workaround on:
-
-    DEBUG_CLR_KERNARG_HDP_FLUSH_WA=1   (no measurable launch cost)
-
-and leaves packet capture at the runtime default.  A user who sets
-DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 keeps the old, slower behaviour.
-
-The runtime reads these variables once, when it initialises.  If the process initialised HIP
-before importing mazero_amd without them, SampledMCTS runs its loop eagerly (GRAPHS_SAFE False).
+The runtime reads the variable once, when it initialises.  If the process initialised HIP before
+importing mazero_amd without setting it, search graphs are not safe to replay and SampledMCTS runs
+its loop eagerly instead (GRAPHS_SAFE is False).
 """
 from __future__ import annotations
 
 import os
 import sys
 
-KEY = "DEBUG_CLR_KERNARG_HDP_FLUSH_WA"
-KEY_CAPTURE = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+KEY = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
 
 
 def _hip_initialised() -> bool:
@@ -43,9 +37,8 @@ def _hip_initialised() -> bool:
 
 
 _user = os.environ.get(KEY)
-_user_capture = os.environ.get(KEY_CAPTURE)
 _late = _hip_initialised()
-os.environ.setdefault(KEY, "1")
-GRAPHS_SAFE = (_user == "1") or (_user_capture == "0") or (_user is None and not _late)
+os.environ.setdefault(KEY, "0")
+GRAPHS_SAFE = (_user == "0") or (_user is None and not _late)
 if os.environ.get("MZ_GRAPH_ENV_EXPERIMENT") == "1":  # diagnostics: other runtime settings under test
     GRAPHS_SAFE = True

@@ -204,7 +204,7 @@ class SampledMCTS:
         self._lib = lib
         if use_graph and not _hipenv.GRAPHS_SAFE:
             warnings.warn("HIP was initialised before mazero_amd was imported without "
-                          "DEBUG_CLR_KERNARG_HDP_FLUSH_WA=1: search graphs are disabled (see mazero_amd/_hipenv.py)")
+                          "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0: search graphs are disabled (see mazero_amd/_hipenv.py)")
             use_graph = False
         self.use_graph = use_graph
 
