@@ -204,6 +204,8 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 __device__ __forceinline__ float unif(float v) { return i2f(uni(f2i(v))); }
 __device__ __forceinline__ int4 uni4(int4 v) { return make_int4(uni(v.x), uni(v.y), uni(v.z), uni(v.w)); }
 __device__ __forceinline__ int rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+// lane l of v := x (l, x uniform)
+__device__ __forceinline__ int wl(int v, int x, int l) { return (lane_id() == l) ? x : v; }
 __device__ __forceinline__ float rlf(float v, int l) { return i2f(__builtin_amdgcn_readlane(f2i(v), l)); }
 __device__ __forceinline__ double rld(double v, int l) {
     const long long b = __double_as_longlong(v);
@@ -408,6 +410,12 @@ __device__ __forceinline__ unsigned rng_word_lane(const Geo &g, const Dev &d, co
         return 0u;
     }
     return d.R()[(size_t)t * g.W + idx];
+}
+
+// RNG word `idx` (per lane) from the LDS window only (0 outside it: select_word checks the range)
+__device__ __forceinline__ unsigned rng_word_win(const unsigned *win, int wbase, int idx) {
+    const int o = idx - wbase;
+    return (o >= 0 && o < kRngWin) ? win[o] : 0u;
 }
 
 // std::discrete_distribution<int>::param_type::_M_initialize (libstdc++ random.tcc:2656-2690) for
@@ -1141,7 +1149,8 @@ __device__ __forceinline__ float puct(const Geo &g, const Lds &s, int n, int v) 
 
 // value part of ucb_score for every node (cnode.cpp:317-331): qsa - parent.pred_value (0 while
 // unvisited), min/max normalised, clamped to [0, 1].  One float division per node, all nodes in
-// parallel, so the walk itself only multiplies and adds.
+// parallel.  General trees also get the whole ucb_score under the parent (Sc), which the tie lists
+// of select_walk read.
 __device__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const TreeHdr &h) {
     const int l = lane_id();
     const bool mm_on = h.mm_cnt > 0;
@@ -1161,8 +1170,8 @@ __device__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const Tr
             if (vs > 1) vs = 1;
             s.Vs[n] = vs;
             if (g.K > 1 && n >= 1) {
-                // ucb_score under the parent (cnode.cpp:297-335), as the walk would compute it;
-                // a parent outside the pUCT table range is reported by the walk itself
+                // ucb_score under the parent (cnode.cpp:297-335); a parent outside the pUCT table
+                // range is reported by its tie list (select_walk)
                 const int np = s.A[s.Par[n]].x - 1;  // total_children_visit_counts
                 s.Sc[n] = (np >= 0 && np < g.PS) ? puct(g, s, np, a4.x) * i2f(a4.y) + vs : 0.f;
             }
@@ -1173,10 +1182,14 @@ __device__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const Tr
 
 __device__ __forceinline__ unsigned select_word(const Geo &g, const Dev &d, const Lds &s, int t, int cursor, int wbase,
                                                 int lds_base, unsigned rw0, unsigned rw1, int &err) {
-    const int o = cursor - wbase;
-    if (o >= 0 && o < kWave) return (unsigned)rl((int)rw0, o);
-    if (o >= kWave && o < 2 * kWave) return (unsigned)rl((int)rw1, o - kWave);
-    if (cursor - lds_base >= 0 && cursor - lds_base < kRngWin) return (unsigned)uni((int)s.rng[cursor - lds_base]);
+    // rw0 / rw1 hold words wbase + [0, 128) copied from the LDS window only (rng_word_win), so
+    // reading them waits for LDS, never for the expansion's outstanding stores
+    const int o = cursor - wbase, ol = cursor - lds_base;
+    if (ol >= 0 && ol < kRngWin) {
+        if (o >= 0 && o < kWave) return (unsigned)rl((int)rw0, o);
+        if (o >= kWave && o < 2 * kWave) return (unsigned)rl((int)rw1, o - kWave);
+        return (unsigned)uni((int)s.rng[ol]);
+    }
     if (cursor < g.W) return (unsigned)uni((int)d.R()[(size_t)t * g.W + cursor]);
     err |= kErrRng;
     return 0u;
@@ -1201,15 +1214,14 @@ __device__ __forceinline__ float path_score(const Geo &g, const Lds &s, int pare
 // (score >= FLOAT_MIN, not NaN), which decides whether an engine word is consumed: all levels
 // are scored in parallel and the words counted with one ballot.
 //
-// Otherwise the walk goes level by level in LDS.  Lane j scores child j; the sequential arg-max
-// with epsilon ties (list = [r] + {i > r : s_i >= M - eps}, M the max and r its first index)
-// becomes a DPP max and two ballots; one engine word when the list is non-empty.  A single-child
-// level takes child 0 whatever the score, so it is walked speculatively (one word assumed) and
-// its score checked in parallel afterwards; a failed check re-walks exactly.
+// Otherwise select_child (its tie list: the sequential arg-max with epsilon ties) is evaluated for
+// every internal node at once, one lane per node, before the walk; the walk then descends one LDS
+// round trip per level and spends serial work only on the engine word (one per non-forced level
+// with a non-empty list; the pick among several tied children takes it modulo the list size).
 // --------------------------------------------------------------------------------------------
 __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base,
                             unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl,
-                            bool fast) {
+                            bool fast, float disc) {
     const int l = lane_id();
     const int cursor0 = h.cursor;
     const int wbase = cursor0;  // register window [wbase, wbase + 128)
@@ -1260,144 +1272,167 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
         return;
     }
 
-    int x = 0, D = 0, cursor = cursor0, phsx = 0;
-    int4 xa = make_int4(0, 0, 0, 0), xb = xa;
 #ifdef MZ_PROBE3
-    const unsigned long long q0 = __builtin_amdgcn_s_memtime();
-    unsigned long long q1 = q0, q2 = q0;
-    int attempts = 0;
+    unsigned long long q0 = __builtin_amdgcn_s_memtime(), q1 = 0, q2 = 0, q3 = 0;
 #endif
-    for (int attempt = 0; attempt < 2; ++attempt) {
+    // (1) internal nodes (children count > 0), compacted into s.boot (free once the
+    // back-propagation is done); every other node gets the walk's stop mark (s.Par: the parent
+    // indices are not needed after value_scores)
+    constexpr int kNxtLeaf = -1, kNxtSlow = -2;
+    int *ilist = (int *)s.boot;
+    int *nxt = s.Par;
+    int nint = 0;
+    for (int base = 0; base < tot; base += kWave) {
+        const int n = base + l;
+        const bool in = n < tot && nc_of(s.B[n].y) > 0;
+        const unsigned long long m = ballot(in);
+        if (in) ilist[nint + __popcll(m & ((1ull << l) - 1ull))] = n;
+        else if (n < tot) nxt[n] = kNxtLeaf;
+        nint += __popcll(m);
+    }
+    wait_lds();
 #ifdef MZ_PROBE3
-        ++attempts;
+    q1 = __builtin_amdgcn_s_memtime();
 #endif
-        const bool spec = (attempt == 0);
-        x = 0;
-        D = 0;
-        cursor = cursor0;
-        xa = uni4(s.A[0]);
-        xb = uni4(s.B[0]);
-        phsx = xb.w;
-        scored = 0;
-        if (l == 0) {
-            s.path[0] = make_int2(0, xa.x);
-            s.flag[0] = 0;
+    // (2) select_child's tie list of every internal node (cnode.cpp:355-370), one lane per node,
+    // over its children's scores (value_scores): the reference's sequential arg-max with epsilon
+    // ties.  A one-child list (the usual case) is stored as the next node; other lists go to the
+    // record {bits lo (Vs), bits hi (flag), size | table error << 16 (Q)} for the exact path (the
+    // walk reads no node's Vs / flag / Q otherwise; Q is re-staged from HBM by the next launch).
+    for (int j0 = 0; j0 < nint; j0 += kWave) {
+        const int j = j0 + l;
+        if (j < nint) {
+            const int p = ilist[j];
+            const int pv = s.A[p].x;
+            const int4 pbn = s.B[p];
+            const int fc = pbn.x, nc = nc_of(pbn.y);
+            const int np = pv - 1;  // total_children_visit_counts = node->visit_count - 1
+            const bool terr = np < 0 || np >= g.PS;
+            float mx = -1000000.0f;  // FLOAT_MIN (utils.h:12)
+            unsigned long long lst = 0ull;
+            int cnt = 0;
+            for (int i0 = 0; i0 < nc; i0 += 4) {
+                float sc[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) sc[u] = s.Sc[fc + ((i0 + u < nc) ? i0 + u : i0)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + u;
+                    if (i < nc) {
+                        if (mx < sc[u]) {
+                            mx = sc[u];
+                            lst = 1ull << i;
+                            cnt = 1;
+                        } else if (sc[u] >= mx - 0.000001f) {
+                            lst |= 1ull << i;
+                            ++cnt;
+                        }
+                    }
+                }
+            }
+            if (cnt == 1 && !terr) {
+                nxt[p] = fc + __builtin_ctzll(lst);
+            } else {
+                nxt[p] = kNxtSlow;
+                s.Vs[p] = i2f((int)(unsigned)(lst & 0xffffffffull));
+                s.flag[p] = (int)(unsigned)(lst >> 32);
+                s.Q[p] = i2f(cnt | (terr ? 0x10000 : 0));
+            }
+        }
+    }
+    wait_lds();
+#ifdef MZ_PROBE3
+    q2 = __builtin_amdgcn_s_memtime();
+#endif
+    // (3) the walk: one LDS read per level (the next node), one engine word per level; the
+    // exact record only for ties, empty lists and table errors.  Level i's node goes to lane i of
+    // px (LDS beyond 64 levels).
+    int x = 0, D = 0, cursor = cursor0;
+    int px = 0;
+    {
+        const int4 r0b = uni4(s.B[0]);
+        const int rv = uni(s.A[0].x);
+        const int nc0 = nc_of(r0b.y);
+        int v;
+        if (nc0 > 0 && rv <= nc0) {
+            v = r0b.x + rv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
+        } else {
+            v = uni(nxt[0]);
+            if (v >= 0) ++cursor;
         }
         while (true) {
-#ifdef MZ_PROBE3
-            const unsigned long long lv0 = __builtin_amdgcn_s_memtime();
-#endif
-            x = uni(x);
-            D = uni(D);
-            cursor = uni(cursor);
-            xa = uni4(xa);
-            xb = uni4(xb);
-            const int nc = nc_of(xb.y);
-            if (nc == 0) break;
-            const int fc = xb.x;
-            const bool has = l < nc;
-            int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
-            if (has) {
-                ca = s.A[fc + l];
-                cb = s.B[fc + l];
-            }
-#ifdef MZ_PROBE3
-            wait_lds();
-            const unsigned long long lv1 = __builtin_amdgcn_s_memtime();
-            stl[MZ_S_CYC_W1_ROUND1] += (long long)(lv1 - lv0);  // level head: uniform state + children reads
-#endif
-            int ci = 0, fl = 0;
-            if (x == 0 && xa.x <= nc) {
-                ci = xa.x - 1;  // forced root round-robin (cnode.cpp:398-399)
-            } else if (nc == 1 && spec) {
-                ++cursor;  // select_child of a single child: child 0, one word if its score is valid
-                fl = 1;
-            } else {
-                const int ntot = xa.x - 1;  // total_children_visit_counts = node->visit_count - 1
-                if (ntot < 0 || ntot >= g.PS) {
+            if (v < 0) {
+                if (v == kNxtLeaf) break;
+                // exact path for this level: ties (engine word modulo the list size), an empty
+                // list (child 0, no word) or a table error
+                const int xfl = uni(f2i(s.Q[x]));
+                if (xfl >> 16) {
                     err |= kErrTable;
                     break;
                 }
-                scored += nc;
-                float sc = -INFINITY;
-                if (has) sc = s.Sc[fc + l];  // puct(ntot, visit) * prior + value score, precomputed
-                const float M = wave_max(sc);
-                unsigned long long lst;
-                if (M > -1000000.0f) {
-                    const unsigned long long first = ballot(has && sc == M);
-                    const int r = __builtin_ctzll(first);
-                    lst = ballot(has && sc >= M - 0.000001f) & (~0ull << r);
-                } else {
-                    lst = ballot(has && sc >= -1000000.0f);
-                }
-                const int cnt = __popcll(lst);
+                const int cnt = xfl & 0xffff;
+                int ci = 0;
                 if (cnt > 0) {
-                    const unsigned w = select_word(g, d, s, t, cursor, wbase, lds_base, rw0, rw1, err);
+                    unsigned long long lst = ((unsigned long long)(unsigned)uni(s.flag[x]) << 32) |
+                                             (unsigned)uni(f2i(s.Vs[x]));
+                    if (cnt > 1) {
+                        const unsigned w = select_word(g, d, s, t, cursor, wbase, lds_base, rw0, rw1, err);
+                        for (int k = (int)(w % (unsigned)cnt); k > 0; --k) lst &= lst - 1ull;
+                    }
                     ++cursor;
-                    int k = (cnt == 1) ? 0 : (int)(w % (unsigned)cnt);  // gen() % max_index_lst.size()
-                    for (; k > 0; --k) lst &= lst - 1ull;
                     ci = __builtin_ctzll(lst);
                 }
+                v = uni(s.B[x].x) + ci;
             }
-            // descend
-#ifdef MZ_PROBE3
-            const unsigned long long lv2 = __builtin_amdgcn_s_memtime();
-            stl[MZ_S_CYC_W1_STAGE2] += (long long)(lv2 - lv1);  // score, arg-max, tie word
-#endif
-            phsx = xb.w;
-            x = fc + ci;
-            xa = make_int4(rl(ca.x, ci), rl(ca.y, ci), rl(ca.z, ci), rl(ca.w, ci));
-            xb = make_int4(rl(cb.x, ci), rl(cb.y, ci), rl(cb.z, ci), rl(cb.w, ci));
             if (D + 1 >= g.PS) {
                 err |= kErrPath;
                 break;
             }
+            x = v;
             ++D;
-            if (l == 0) {
-                s.path[D] = make_int2(x, xa.x);
-                s.flag[D] = fl;
-            }
-#ifdef MZ_PROBE3
-            stl[MZ_S_CYC_W1_BACKUP] += (long long)(__builtin_amdgcn_s_memtime() - lv2);  // descend
-#endif
+            if (D < kWave) px = wl(px, x, D);
+            else if (l == 0) s.path[D].x = x;
+            v = uni(nxt[x]);
+            if (v >= 0) ++cursor;
         }
-#ifdef MZ_PROBE3
-        q1 = __builtin_amdgcn_s_memtime();
-#endif
-        if (!spec) break;
-        // verify the speculated single-child levels in parallel
-        wait_lds();
-        bool bad = false;
-        for (int base = 1; base <= D; base += kWave) {
-            const int i = base + l;
-            bool b = false;
-            if (i <= D && s.flag[i]) {
-                const float sc = path_score(g, s, s.path[i - 1].x, s.path[i].x, err);
-                b = !(sc >= -1000000.0f);
-            }
-            bad = bad || (ballot(b) != 0ull);
-        }
-        if (!bad) break;
     }
+    if (cursor > g.W) err |= kErrRng;  // a consumed word beyond the stream (select_word's check)
     if (D == 0) err |= kErrRoot;
+    wait_lds();
+    // the path {node, visit at selection} for the next back-propagation, the statistics and the
+    // outputs, by the whole wave
+    int2 *gp = d.path() + (size_t)t * g.PS;
+    int nsc = 0;
+    int xpar = 0;
+    for (int i0 = 0; i0 <= D; i0 += kWave) {
+        const int i = i0 + l;
+        if (i <= D) {
+            const int xi = (i < kWave) ? px : s.path[i].x;
+            const int2 e = make_int2(xi, s.A[xi].x);
+            gp[i] = e;
+            s.path[i] = e;
+            const int4 bi = s.B[xi];
+            if (i < D && !(i == 0 && e.y <= nc_of(bi.y))) nsc += nc_of(bi.y);  // scored levels
+            if (i == D - 1) xpar = bi.w;
+        }
+    }
+    scored = wave_sum(nsc);
     h.cursor = cursor;
     h.D = D;
     h.leaf = x;
-    out_idx = phsx;          // parent->hidden_state_index_x
-    out_act = act_of(xb.y);  // children_action of the last edge
+    out_idx = uni(rl(xpar, (D - 1) & (kWave - 1)));  // parent->hidden_state_index_x
+    if (D == 0) out_idx = uni(s.B[0].w);
+    out_act = act_of(uni(s.B[x].y));  // children_action of the last edge
     stl[MZ_S_SELECTS] += 1;
     stl[MZ_S_PATH_EDGES] += D;
     stl[MZ_S_SCORED] += scored;
-    wait_lds();
 #ifdef MZ_PROBE3
-    q2 = __builtin_amdgcn_s_memtime();
-    stl[MZ_S_CYC_EXP_DRAW] += (long long)(q1 - q0);    // walk (last attempt's descent)
-    stl[MZ_S_CYC_EXP_NODES] += (long long)(q2 - q1);   // speculation check
-    stl[MZ_S_CYC_W1_SYNC] += attempts + 100 * D;
+    q3 = __builtin_amdgcn_s_memtime();
+    stl[MZ_S_CYC_W1_ROUND1] += (long long)(q1 - q0);  // compaction
+    stl[MZ_S_CYC_W1_STAGE2] += (long long)(q2 - q1);  // tie lists
+    stl[MZ_S_CYC_W1_BACKUP] += (long long)(q3 - q2);  // walk + path
+    stl[MZ_S_CYC_W1_SYNC] += nint;
 #endif
-    // publish the path {node, visit} for the next back-propagation
-    int2 *gp = d.path() + (size_t)t * g.PS;
-    for (int i = l; i <= D; i += kWave) gp[i] = s.path[i];
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1802,11 +1837,16 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         stl[MZ_S_CYC_EXP_CDF] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // value scores
 #endif
         // register RNG window: words h.cursor + [0, 128) (select's words follow the expansion's)
-        int perr = 0;  // words past the stream end only matter if the walk consumes them
-        const unsigned rw0 = fast ? 0u : rng_word_lane(g, d, s.rng, wbase, t, h.cursor + l, perr);
-        const unsigned rw1 = fast ? 0u : rng_word_lane(g, d, s.rng, wbase, t, h.cursor + kWave + l, perr);
+        const unsigned rw0 = fast ? 0u : rng_word_win(s.rng, wbase, h.cursor + l);
+        const unsigned rw1 = fast ? 0u : rng_word_win(s.rng, wbase, h.cursor + kWave + l);
         int idx = 0, act = 0;
-        select_walk(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast);
+#ifdef MZ_PROBE3
+        wait_vm();
+        wait_lds();
+        asm volatile("" ::"v"(rw0), "v"(rw1));
+        stl[MZ_S_CYC_EXP_DRAW] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // up to the walk
+#endif
+        select_walk(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast, a.discount);
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;
@@ -2316,7 +2356,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.oVs = o; o += round16(4 * g.P);
     g.oC = o; o += round16(16 * g.P);
     g.oPath = o; o += round16(8 * g.PS);
-    g.oFlag = o; o += round16(4 * g.PS);
+    g.oFlag = o; o += round16(4 * (g.P > g.PS ? g.P : g.PS));  // per node: tie-list sizes (select_walk)
     g.oT = o; o += g.use_table ? round16(4 * g.TT) : 0;
     g.oPb = o; o += round16(4 * (g.PS + kWave));
     g.oSq = o; o += round16(8 * (g.PS + kWave));
