@@ -1648,6 +1648,17 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
                            (long long)(uintptr_t)a.gather_out) & 15) == 0) &&
                         a.row_bytes <= 4 * 16 * kWave;
     const bool g_pre = EB && g_fast && g.K == 1;
+    // rows above 4 KiB (27m: 13.5 KiB) are staged through LDS with LDS-DMA (no registers held),
+    // in the value-entry staging area s.reg: free in K = 1 chains for the whole launch (their
+    // updates never read entries) and free in every tree once the back-propagation wave is done
+    unsigned char *sbig = (unsigned char *)s.reg;
+    const long long big_cap = 8ll * (NC > 0 ? kRegCap : g.reg_cap);
+    const bool g_big = SEL && a.pool && !JOINT &&
+                       (((a.row_bytes | a.pool_stride | (long long)(uintptr_t)a.pool |
+                          (long long)(uintptr_t)a.gather_out) & 15) == 0) &&
+                       a.row_bytes > 4 * 16 * kWave && a.row_bytes <= 16 * 16 * kWave && a.row_bytes <= big_cap;
+    const bool g_pre_big = EB && g_big && g.K == 1;
+    bool gath_lds = false;
     long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
     // counters written per launch: the algorithmic ones, plus the cycle stamps in diagnostic builds
     constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
@@ -1665,6 +1676,13 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
         gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else if (wv == 0 && g_pre_big) {
+        // the same for a big row: always sixteen 1 KiB LDS-DMA chunks (clamped), left in flight
+        const char *src = a.pool + (long long)a.hsx * a.pool_stride + (long long)t * a.row_bytes;
+        const long long last = a.row_bytes - 16, o = (long long)l * 16;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) glds16(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     } else {
         wait_vm();
     }
@@ -1866,6 +1884,18 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
                 gath_pending = true;
                 gdst = dst;
                 grb = rb;
+            } else if (g_pre_big && idx == a.hsx) {  // staged in LDS in round 1
+                gath_lds = true;
+                gdst = dst;
+                grb = rb;
+            } else if (g_big) {
+                const long long last = rb - 16, o = (long long)l * 16;
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    glds16(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+                gath_lds = true;
+                gdst = dst;
+                grb = rb;
             } else if (g_fast) {
                 // up to 4 KiB per row: all loads in flight at once, stores after the header write-back
                 const long long o = (long long)l * 16;
@@ -1908,6 +1938,11 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
             hp->tame = h.tame;
             hp->leaf = h.leaf;
         }
+    }
+    if (gath_lds) {
+        wait_vm();  // the LDS-DMA chunks have landed
+        for (long long o = (long long)l * 16; o < grb; o += 16 * kWave)
+            *(int4 *)(gdst + o) = *(const int4 *)(sbig + o);
     }
     if (gath_pending) {
         const long long o = (long long)l * 16;

@@ -151,11 +151,20 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
 
 
-def test_gather_pool(gpu_lib):
-    """Fused leaf hidden-state gather == pool[idx_x[i], i] (mcts_sampled.py:130-134)."""
+@pytest.mark.parametrize("K,H", [
+    (5, 384),    # 1.5 KiB rows (3m): register chunks
+    (1, 384),    # K = 1: the row prefetched in round 1
+    (1, 3456),   # 13.5 KiB rows (27m): LDS-DMA staging, prefetched in round 1
+    (5, 3456),   # 13.5 KiB rows, staged after the selection
+    (1, 1025),   # 4100-byte rows: not 16-byte aligned (dword loop)
+    (5, 5000),   # 20,000-byte rows: above the staging area (plain loop)
+])
+def test_gather_pool(gpu_lib, K, H):
+    """Fused leaf hidden-state gather == pool[idx_x[i], i] (mcts_sampled.py:130-134), over the
+    kernel's row-size classes."""
     from mazero_amd.synthetic import make_search_inputs
 
-    B, A, K, S, H = 64, 9, 5, 20, 384
+    B, A, S = 64, 9, 20
     inp = make_search_inputs(np.random.default_rng(3), B, A, S)
     pool = torch.randn(S + 1, B, H, device="cuda")
     out, gathered = run_fused(make_tb(gpu_lib, inp, K, {}), to_device(inp), K, {}, pool=pool)
@@ -166,9 +175,13 @@ def test_gather_pool(gpu_lib):
     pool16 = pool.half()
     g16 = torch.empty(B, H, dtype=torch.float16, device="cuda")
     tb = make_tb(gpu_lib, inp, K, {})
-    gpu_lib.mz_gather_rows(tb._h, pool16.data_ptr(), pool16.stride(0) * 2, H * 2, idx[3].int().contiguous().data_ptr(),
-                           g16.data_ptr())
+    rc = gpu_lib.mz_gather_rows(tb._h, pool16.data_ptr(), pool16.stride(0) * 2, H * 2,
+                                idx[3].int().contiguous().data_ptr(), g16.data_ptr())
     torch.cuda.synchronize()
+    if (H * 2) % 4:  # the standalone gather copies whole dwords: other row sizes are refused
+        assert rc != 0 and b"multiple of 4" in gpu_lib.mz_last_error()
+        return
+    assert rc == 0
     assert torch.equal(g16, pool16[idx[3], torch.arange(B, device="cuda")])
 
 
