@@ -1396,6 +1396,10 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
             if (v >= 0) ++cursor;
         }
     }
+#ifdef MZ_PROBE3
+    wait_lds();
+    const unsigned long long q2b = __builtin_amdgcn_s_memtime();
+#endif
     if (cursor > g.W) err |= kErrRng;  // a consumed word beyond the stream (select_word's check)
     if (D == 0) err |= kErrRoot;
     wait_lds();
@@ -1431,7 +1435,7 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
     stl[MZ_S_CYC_W1_ROUND1] += (long long)(q1 - q0);  // compaction
     stl[MZ_S_CYC_W1_STAGE2] += (long long)(q2 - q1);  // tie lists
     stl[MZ_S_CYC_W1_BACKUP] += (long long)(q3 - q2);  // walk + path
-    stl[MZ_S_CYC_W1_SYNC] += nint;
+    stl[MZ_S_CYC_W1_SYNC] += (long long)(q2b - q2);  // walk loop only
 #endif
 }
 

@@ -151,6 +151,20 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
 
 
+@pytest.mark.parametrize("B,A,K,S", [(256, 9, 5, 50), (128, 15, 10, 100), (64, 3, 10, 60)])
+def test_ties_vs_port(gpu_lib, port_lib, B, A, K, S):
+    """Uniform policies and zero rewards/values: children with equal priors tie in select_child
+    (cnode.cpp:355-370), so the walk breaks ties with engine words (gen() % list size) on many
+    levels -- the exact record path of select_walk, at full batch sizes."""
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    inp = make_search_inputs(np.random.default_rng(B * 1000 + K), B, A, S, ties=True)
+    exp = run_search(make_tb(port_lib, inp, K, {}), inp, K, {})
+    out, _ = run_fused(make_tb(gpu_lib, inp, K, {}), to_device(inp), K, {})
+    exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, exp, f"gpu ties B={B} A={A} K={K} ")
+
+
 @pytest.mark.parametrize("K,H", [
     (5, 384),    # 1.5 KiB rows (3m): register chunks
     (1, 384),    # K = 1: the row prefetched in round 1
