@@ -1360,29 +1360,33 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
             v = uni(nxt[0]);
             if (v >= 0) ++cursor;
         }
+        // (every branch condition and loop-carried value goes through readfirstlane, so the
+        // compiler keeps the loop on the scalar unit instead of an exec-masked loop)
         while (true) {
+            v = uni(v);
+            cursor = uni(cursor);
             if (v < 0) {
                 if (v == kNxtLeaf) break;
                 // exact path for this level: ties (engine word modulo the list size), an empty
                 // list (child 0, no word) or a table error
                 const int xfl = uni(f2i(s.Q[x]));
-                if (xfl >> 16) {
+                if (uni(xfl >> 16)) {
                     err |= kErrTable;
                     break;
                 }
-                const int cnt = xfl & 0xffff;
+                const int cnt = uni(xfl & 0xffff);
                 int ci = 0;
                 if (cnt > 0) {
                     unsigned long long lst = ((unsigned long long)(unsigned)uni(s.flag[x]) << 32) |
                                              (unsigned)uni(f2i(s.Vs[x]));
                     if (cnt > 1) {
                         const unsigned w = select_word(g, d, s, t, cursor, wbase, lds_base, rw0, rw1, err);
-                        for (int k = (int)(w % (unsigned)cnt); k > 0; --k) lst &= lst - 1ull;
+                        for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
                     }
                     ++cursor;
-                    ci = __builtin_ctzll(lst);
+                    ci = uni(__builtin_ctzll(lst));
                 }
-                v = uni(s.B[x].x) + ci;
+                v = uni(uni(s.B[x].x) + ci);
             }
             if (D + 1 >= g.PS) {
                 err |= kErrPath;
