@@ -488,7 +488,7 @@ __device__ __forceinline__ double cdf_lane(double bd, int A) {
 // Creates the children in HBM (and in the LDS mirrors when given), advances cursor / tot and
 // returns nc.  `pv` is the expanded node's pred_value (the children's PP).
 // --------------------------------------------------------------------------------------------
-__device__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float pol, float bet, float noi, float eps,
+__device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float pol, float bet, float noi, float eps,
                            int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
                            long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl, int &wild) {
     const int l = lane_id();
@@ -872,7 +872,7 @@ __device__ __forceinline__ void boot_dpp(float &b, float &tmp, float dv, float r
 // chains).  Chunks hold <= 64 nodes whose needed entries fit g.reg_cap.  Returns cnt (uniform);
 // lane l gets its node id, entry count (= visit at selection), need flag and staging offset.
 // --------------------------------------------------------------------------------------------
-__device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &need,
+__device__ __forceinline__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &need,
                              int &off) {
     const int l = lane_id();
     const int i = i0 + l;
@@ -930,7 +930,7 @@ __device__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, i
 // 79-103) is recomputed as a reduction over the q of every visited non-root node -- exactly the
 // multiset's content.  Chunk 0's entries must already be in flight (stage_regions).
 // --------------------------------------------------------------------------------------------
-__device__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float reward, float disc,
+__device__ __forceinline__ void backup(const Geo &g, const Dev &d, Lds &s, int t, int D, int tot, float value, float reward, float disc,
                        TreeHdr &h, int cnt0, int n0, int nv0, int need0, int off0, int &err, long long *stl,
                        float *xmm) {
     const int l = lane_id();
@@ -1151,7 +1151,7 @@ __device__ __forceinline__ float puct(const Geo &g, const Lds &s, int n, int v) 
 // unvisited), min/max normalised, clamped to [0, 1].  One float division per node, all nodes in
 // parallel.  General trees also get the whole ucb_score under the parent (Sc), which the tie lists
 // of select_walk read.
-__device__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const TreeHdr &h) {
+__device__ __forceinline__ void value_scores(const Geo &g, Lds &s, int tot, float disc, const TreeHdr &h) {
     const int l = lane_id();
     const bool mm_on = h.mm_cnt > 0;
     const float mmn = h.mm_min, mmx = h.mm_max;
@@ -1206,72 +1206,19 @@ __device__ __forceinline__ float path_score(const Geo &g, const Lds &s, int pare
     return puct(g, s, n, ca.x) * i2f(ca.y) + s.Vs[child];
 }
 
-// --------------------------------------------------------------------------------------------
-// CTree::select_path (cnode.cpp:381-413) with select_child (337-379) and ucb_score (297-335).
-//
-// K = 1 trees are chains (one child per expansion), so the path is every node in creation order
-// and the only data-dependent effect of a level is whether select_child's tie list is non-empty
-// (score >= FLOAT_MIN, not NaN), which decides whether an engine word is consumed: all levels
-// are scored in parallel and the words counted with one ballot.
-//
-// Otherwise select_child (its tie list: the sequential arg-max with epsilon ties) is evaluated for
-// every internal node at once, one lane per node, before the walk; the walk then descends one LDS
-// round trip per level and spends serial work only on the engine word (one per non-forced level
-// with a non-empty list; the pick among several tied children takes it modulo the list size).
-// --------------------------------------------------------------------------------------------
-__device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base,
-                            unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl,
-                            bool fast, float disc) {
-    const int l = lane_id();
-    const int cursor0 = h.cursor;
-    const int wbase = cursor0;  // register window [wbase, wbase + 128)
-    long long scored = 0;
-    if (g.K == 1) {
-        const int D = tot - 1;
-        if (D < 1) err |= kErrRoot;
-        if (D + 1 > g.PS) err |= kErrPath;
-        int words = 0;
-        if (!err) {
-            const int root_visit = uni(s.A[0].x);
-            if (fast) {
-                // Every level's tie list is non-empty: the pUCT coefficients are finite and >= 0
-                // (fast_ok), priors lie in [0, 1e30] and rewards / values in [-1e30, 1e30]
-                // (TreeHdr::tame), so with |discount| <= 1, 0 <= lambda <= 1 and delta_lb > 0 every
-                // q, min/max bound and normalised value is finite, the value score lies in [0, 1]
-                // and the score prior_score + value_score is >= 0 (+inf at worst), never NaN.
-                // Each level consumes one word except the forced root child (cnode.cpp:398-399).
-                // Parent visit totals stay below the table size (root visits <= S + 1 < PS).
-                if (root_visit - 1 >= g.PS) err |= kErrTable;
-                words = D - ((root_visit <= 1) ? 1 : 0);
-            } else {
-                for (int base = 0; base <= D; base += kWave) {
-                    const int i = base + l;
-                    bool valid = false;
-                    if (i <= D) {
-                        if (i >= 1 && !(i == 1 && root_visit <= 1)) {
-                            const float sc = path_score(g, s, i - 1, i, err);
-                            valid = sc >= -1000000.0f;  // tie list non-empty (FLOAT_MIN, utils.h:12)
-                        }
-                    }
-                    words += __popcll(ballot(valid));
-                }
-            }
-            scored = D;
-        }
-        h.cursor = cursor0 + words;
-        h.D = D;
-        h.leaf = D;
-        const int4 pb = uni4(s.B[D > 0 ? D - 1 : 0]);
-        const int4 lb = uni4(s.B[D > 0 ? D : 0]);
-        out_idx = pb.w;
-        out_act = act_of(lb.y);
-        stl[MZ_S_SELECTS] += 1;
-        stl[MZ_S_PATH_EDGES] += D;
-        stl[MZ_S_SCORED] += scored;
-        // (no path record: the next back-propagation walks the chain itself, stage_regions)
-        return;
-    }
+// Layout classes up to this pool size take the precomputed walk (cheaper while the per-node
+// scoring passes are few); larger classes and the general layout take the level walk (measured:
+// 3m K = 5 in class 512 12.0 against 12.8 us, 27m K = 5 in class 1024 15.8 against 19.1 us).  A
+// compile-time choice: with both walks in one kernel the compiler kept the LDS view in scratch.
+template <int NC>
+constexpr bool kWalkPrecomputed = (NC > 0 && NC <= 512);
 
+// General trees, small pools: select_child resolved for every internal node first (scores per
+// node by value_scores, one lane per internal node for the tie lists), then a pointer chase.
+__device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base, unsigned rw0, unsigned rw1,
+                            int &err, int &out_idx, int &out_act, long long *stl, float disc, int cursor0, int wbase) {
+    const int l = lane_id();
+    long long scored = 0;
 #ifdef MZ_PROBE3
     unsigned long long q0 = __builtin_amdgcn_s_memtime(), q1 = 0, q2 = 0, q3 = 0;
 #endif
@@ -1443,6 +1390,209 @@ __device__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, 
 #endif
 }
 
+// General trees, large pools: level by level, each level's children scored on the fly.
+__device__ __forceinline__ void walk_levels(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base, unsigned rw0, unsigned rw1,
+                            int &err, int &out_idx, int &out_act, long long *stl, float disc, int cursor0, int wbase) {
+    const int l = lane_id();
+#ifdef MZ_PROBE3
+    const unsigned long long q0 = __builtin_amdgcn_s_memtime();
+#endif
+    // General trees: level by level, select_child (cnode.cpp:337-379) scored on the fly, lane j
+    // for child j, with ucb_score's arithmetic (cnode.cpp:297-335).  The reference's sequential
+    // arg-max with epsilon ties is the closed form [r] + {i > r : s_i >= M - eps} (M the maximum,
+    // r its first index; {i : s_i >= FLOAT_MIN} when M <= FLOAT_MIN): a row / wave max and two
+    // ballots.  Every branch condition and loop-carried value goes through readfirstlane, so
+    // the loop stays on the scalar unit.  Level i's node goes to lane i of px (LDS past 64).
+    const bool mm_on = h.mm_cnt > 0;
+    const float mmn = h.mm_min, mmx = h.mm_max;
+    float den = 0.f;
+    if (mm_on) {
+        const float delta = mmx - mmn;
+        den = (g.delta < delta) ? delta : g.delta;  // std::max(delta_lb, delta)
+    }
+    int x = 0, D = 0, cursor = cursor0;
+    int px = 0;
+    int xv = uni(s.A[0].x);
+    int4 xb = uni4(s.B[0]);
+    long long nscored = 0;
+    while (true) {
+        x = uni(x);
+        xv = uni(xv);
+        cursor = uni(cursor);
+        const int nc = uni(nc_of(xb.y));
+        if (nc == 0) break;
+        const int fc = uni(xb.x);
+        int ci = 0;
+        if (x == 0 && xv <= nc) {
+            ci = xv - 1;  // forced root round-robin (cnode.cpp:398-399)
+        } else {
+            const int np = xv - 1;  // total_children_visit_counts = node->visit_count - 1
+            if (np < 0 || np >= g.PS) {
+                err |= kErrTable;
+                break;
+            }
+            nscored += nc;
+            const bool has = l < nc;
+            float sc = -INFINITY;
+            if (has) {
+                const int4 ca = s.A[fc + l];
+                float vs = (ca.x == 0) ? 0.0f : ((i2f(ca.w) + disc * i2f(ca.z)) - s.PP[fc + l]);
+                if (mm_on) vs = (vs - mmn) / den;
+                if (vs < 0) vs = 0;
+                if (vs > 1) vs = 1;
+                sc = puct(g, s, np, ca.x) * i2f(ca.y) + vs;
+            }
+            float M;
+            if (nc <= 16) {  // one DPP row holds every child
+                float v = sc;
+                v = fmaxf(v, i2f(dpp<0xB1>(f2i(v))));
+                v = fmaxf(v, i2f(dpp<0x4E>(f2i(v))));
+                v = fmaxf(v, i2f(dpp<0x141>(f2i(v))));
+                v = fmaxf(v, i2f(dpp<0x140>(f2i(v))));
+                M = unif(v);
+            } else {
+                M = unif(wave_max(sc));
+            }
+            unsigned long long lst;
+            if (M > -1000000.0f) {  // FLOAT_MIN (utils.h:12)
+                const unsigned long long first = ballot(has && sc == M);
+                const int r = uni(__builtin_ctzll(first));
+                lst = ballot(has && sc >= M - 0.000001f) & (~0ull << r);
+            } else {
+                lst = ballot(has && sc >= -1000000.0f);
+            }
+            const int cnt = uni(__popcll(lst));
+            if (cnt > 0) {  // one engine word (gen() % size); its value matters only for ties
+                if (cnt > 1) {
+                    const unsigned w = select_word(g, d, s, t, cursor, wbase, lds_base, rw0, rw1, err);
+                    for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
+                } else if (cursor >= g.W) {
+                    err |= kErrRng;
+                }
+                ++cursor;
+                ci = uni(__builtin_ctzll(lst));
+            }
+        }
+        if (D + 1 >= g.PS) {
+            err |= kErrPath;
+            break;
+        }
+        x = uni(fc + ci);
+        ++D;
+        if (D < kWave) px = wl(px, x, D);
+        else if (l == 0) s.path[D].x = x;
+        xv = uni(s.A[x].x);
+        xb = uni4(s.B[x]);
+    }
+    if (D == 0) err |= kErrRoot;
+    wait_lds();
+#ifdef MZ_PROBE3
+    const unsigned long long q1 = __builtin_amdgcn_s_memtime();
+#endif
+    // the path {node, visit at selection} for the next back-propagation and the outputs, by the
+    // whole wave
+    int2 *gp = d.path() + (size_t)t * g.PS;
+    int xpar = 0;
+    for (int i0 = 0; i0 <= D; i0 += kWave) {
+        const int i = i0 + l;
+        if (i <= D) {
+            const int xi = (i < kWave) ? px : s.path[i].x;
+            const int2 e = make_int2(xi, s.A[xi].x);
+            gp[i] = e;
+            s.path[i] = e;
+            if (i == D - 1) xpar = s.B[xi].w;
+        }
+    }
+    h.cursor = cursor;
+    h.D = D;
+    h.leaf = x;
+    out_idx = (D == 0) ? uni(s.B[0].w) : uni(rl(xpar, (D - 1) & (kWave - 1)));  // parent->hidden_state_index_x
+    out_act = act_of(uni(s.B[x].y));  // children_action of the last edge
+    stl[MZ_S_SELECTS] += 1;
+    stl[MZ_S_PATH_EDGES] += D;
+    stl[MZ_S_SCORED] += nscored;
+#ifdef MZ_PROBE3
+    const unsigned long long q2 = __builtin_amdgcn_s_memtime();
+    stl[MZ_S_CYC_W1_ROUND1] += 0;
+    stl[MZ_S_CYC_W1_STAGE2] += 0;
+    stl[MZ_S_CYC_W1_BACKUP] += (long long)(q2 - q0);  // walk + path
+    stl[MZ_S_CYC_W1_SYNC] += (long long)(q1 - q0);    // walk loop only
+#endif
+}
+
+// --------------------------------------------------------------------------------------------
+// CTree::select_path (cnode.cpp:381-413) with select_child (337-379) and ucb_score (297-335).
+//
+// K = 1 trees are chains (one child per expansion), so the path is every node in creation order
+// and the only data-dependent effect of a level is whether select_child's tie list is non-empty
+// (score >= FLOAT_MIN, not NaN), which decides whether an engine word is consumed: all levels
+// are scored in parallel and the words counted with one ballot.
+//
+// Otherwise select_child (its tie list: the sequential arg-max with epsilon ties) is evaluated for
+// every internal node at once, one lane per node, before the walk; the walk then descends one LDS
+// round trip per level and spends serial work only on the engine word (one per non-forced level
+// with a non-empty list; the pick among several tied children takes it modulo the list size).
+// --------------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base,
+                            unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl,
+                            bool fast, float disc) {
+    const int l = lane_id();
+    const int cursor0 = h.cursor;
+    const int wbase = cursor0;  // register window [wbase, wbase + 128)
+    long long scored = 0;
+    if (g.K == 1) {
+        const int D = tot - 1;
+        if (D < 1) err |= kErrRoot;
+        if (D + 1 > g.PS) err |= kErrPath;
+        int words = 0;
+        if (!err) {
+            const int root_visit = uni(s.A[0].x);
+            if (fast) {
+                // Every level's tie list is non-empty: the pUCT coefficients are finite and >= 0
+                // (fast_ok), priors lie in [0, 1e30] and rewards / values in [-1e30, 1e30]
+                // (TreeHdr::tame), so with |discount| <= 1, 0 <= lambda <= 1 and delta_lb > 0 every
+                // q, min/max bound and normalised value is finite, the value score lies in [0, 1]
+                // and the score prior_score + value_score is >= 0 (+inf at worst), never NaN.
+                // Each level consumes one word except the forced root child (cnode.cpp:398-399).
+                // Parent visit totals stay below the table size (root visits <= S + 1 < PS).
+                if (root_visit - 1 >= g.PS) err |= kErrTable;
+                words = D - ((root_visit <= 1) ? 1 : 0);
+            } else {
+                for (int base = 0; base <= D; base += kWave) {
+                    const int i = base + l;
+                    bool valid = false;
+                    if (i <= D) {
+                        if (i >= 1 && !(i == 1 && root_visit <= 1)) {
+                            const float sc = path_score(g, s, i - 1, i, err);
+                            valid = sc >= -1000000.0f;  // tie list non-empty (FLOAT_MIN, utils.h:12)
+                        }
+                    }
+                    words += __popcll(ballot(valid));
+                }
+            }
+            scored = D;
+        }
+        h.cursor = cursor0 + words;
+        h.D = D;
+        h.leaf = D;
+        const int4 pb = uni4(s.B[D > 0 ? D - 1 : 0]);
+        const int4 lb = uni4(s.B[D > 0 ? D : 0]);
+        out_idx = pb.w;
+        out_act = act_of(lb.y);
+        stl[MZ_S_SELECTS] += 1;
+        stl[MZ_S_PATH_EDGES] += D;
+        stl[MZ_S_SCORED] += scored;
+        // (no path record: the next back-propagation walks the chain itself, stage_regions)
+        return;
+    }
+
+    if constexpr (kWalkPrecomputed<NC>)
+        walk_precomputed(g, d, s, t, tot, h, lds_base, rw0, rw1, err, out_idx, out_act, stl, disc, cursor0, wbase);
+    else
+        walk_levels(g, d, s, t, tot, h, lds_base, rw0, rw1, err, out_idx, out_act, stl, disc, cursor0, wbase);
+}
+
 // --------------------------------------------------------------------------------------------
 // One simulation step of one tree: [expand + back-propagate (sim s)] -> [select (sim s+1)] ->
 // [gather the selected leaf's parent hidden state].
@@ -1569,7 +1719,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
                 glds16(d.A() + nb + i0 + l, s.A + i0);
                 glds16(d.Bn() + nb + i0 + l, s.B + i0);
                 glds4(d.PP() + nb + i0 + l, s.PP + i0);
-                if (SEL && g.K > 1) glds4(d.Par() + nb + i0 + l, s.Par + i0);  // parents (general walk)
+                if (SEL && kWalkPrecomputed<NC> && g.K > 1) glds4(d.Par() + nb + i0 + l, s.Par + i0);  // parents (general walk)
                 if (EB) {
                     glds4(d.Q() + nb + i0 + l, s.Q + i0);
                     glds16(d.C() + nb + i0 + l, s.C + i0);  // value-set scalars, read by node
@@ -1725,7 +1875,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
                 glds16(d.A() + nb + i0 + l, s.A + i0);
                 glds16(d.Bn() + nb + i0 + l, s.B + i0);
                 glds4(d.PP() + nb + i0 + l, s.PP + i0);
-                if (SEL && g.K > 1) glds4(d.Par() + nb + i0 + l, s.Par + i0);
+                if (SEL && kWalkPrecomputed<NC> && g.K > 1) glds4(d.Par() + nb + i0 + l, s.Par + i0);
                 if (EB) {
                     glds4(d.Q() + nb + i0 + l, s.Q + i0);
                     glds16(d.C() + nb + i0 + l, s.C + i0);
@@ -1858,7 +2008,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         // K = 1 chains of a tame tree (TreeHdr::tame) under tame handle constants select without
         // scoring: no score can be NaN or below FLOAT_MIN there (select_walk)
         const bool fast = !JOINT && g.K == 1 && fast_ok && h.tame && fabsf(a.discount) <= 1.0f;
-        if (!fast) value_scores(g, s, h.tot, a.discount, h);
+        if (!fast && (g.K == 1 || kWalkPrecomputed<NC>)) value_scores(g, s, h.tot, a.discount, h);
 #ifdef MZ_PROBE3
         stl[MZ_S_CYC_EXP_CDF] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // value scores
 #endif
@@ -1872,7 +2022,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         asm volatile("" ::"v"(rw0), "v"(rw1));
         stl[MZ_S_CYC_EXP_DRAW] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // up to the walk
 #endif
-        select_walk(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast, a.discount);
+        select_walk<NC>(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast, a.discount);
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;

@@ -3,7 +3,7 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 out=gpurun_out/iter.jsonl; : > $out
-for args in "--sampled-times 1" "--sampled-times 5" "--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1" "--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5"; do
+for args in "--sampled-times 1" "--sampled-times 5" "--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1" "--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5" "--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5"; do
   timeout -k 10 200 python bench.py --no-cpu $args >> $out 2> gpurun_out/iter.err || exit $?
 done
 python - $out <<'PY'
@@ -19,8 +19,3 @@ for args in "--sampled-times 1" "--map 27m_vs_30m --roots 256 --sims 200 --sampl
 import json; d=json.loads(open('gpurun_out/st.json').read().strip().splitlines()[-1]); pc=d['roofline']['phase_cycles']
 print('stamps', d['config']['map'], d['roofline']['avg_launch_us'], ' '.join(f'{k}={v:.0f}' for k,v in pc.items()))"
 done
-mkdir -p gpurun_out
-MZ_STAMPS=1 MZ_LIB_OVERRIDE=mazero_amd/_build/variant_probe3.so timeout -k 10 200 python bench.py --no-cpu --sampled-times 5 > gpurun_out/probe.jsonl 2> gpurun_out/probe.err || exit $?
-python -c "
-import json; d=json.loads(open('gpurun_out/probe.jsonl').read().strip().splitlines()[-1]); pc=d['roofline']['phase_cycles']
-print('probe K=5', d['roofline']['avg_launch_us'], ' '.join(f'{k}={v:.0f}' for k,v in pc.items()))"
