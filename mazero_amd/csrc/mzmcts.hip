@@ -1207,11 +1207,12 @@ __device__ __forceinline__ float path_score(const Geo &g, const Lds &s, int pare
 }
 
 // Layout classes up to this pool size take the precomputed walk (cheaper while the per-node
-// scoring passes are few); larger classes and the general layout take the level walk (measured:
-// 3m K = 5 in class 512 12.0 against 12.8 us, 27m K = 5 in class 1024 15.8 against 19.1 us).  A
-// compile-time choice: with both walks in one kernel the compiler kept the LDS view in scratch.
+// scoring passes are few); larger classes and the general layout take the level walk.  Measured
+// on one box: 3m K = 5 (260 nodes) 12.0 us precomputed against 12.7 us by levels; 3s5z K = 5 (510
+// nodes) 14.5 against 13.9 us; 27m K = 5 (1010 nodes) 19.1 against 15.8 us.  A compile-time
+// choice: with both walks in one kernel the compiler kept the LDS view in scratch memory.
 template <int NC>
-constexpr bool kWalkPrecomputed = (NC > 0 && NC <= 512);
+constexpr bool kWalkPrecomputed = (NC > 0 && NC <= 384);
 
 // General trees, small pools: select_child resolved for every internal node first (scores per
 // node by value_scores, one lane per internal node for the tie lists), then a pointer chase.
@@ -2423,6 +2424,7 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         case 64: launch_nc<64>(b, eb, sel, a); break;
         case 128: launch_nc<128>(b, eb, sel, a); break;
         case 256: launch_nc<256>(b, eb, sel, a); break;
+        case 384: launch_nc<384>(b, eb, sel, a); break;
         case 512: launch_nc<512>(b, eb, sel, a); break;
         case 1024: launch_nc<1024>(b, eb, sel, a); break;
         default: launch_nc<0>(b, eb, sel, a); break;
@@ -2575,7 +2577,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     g.lds = o;
     // compile-time layout class (pb / sq pUCT tables, value-entry chunks of kRegCap)
     b->nc = 0;
-    for (int nc : {64, 128, 256, 512, 1024})
+    for (int nc : {64, 128, 256, 384, 512, 1024})
         if (b->P <= nc) {
             b->nc = nc;
             break;
@@ -2591,6 +2593,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             case 64: g.lds = Layout<64>::total; break;
             case 128: g.lds = Layout<128>::total; break;
             case 256: g.lds = Layout<256>::total; break;
+            case 384: g.lds = Layout<384>::total; break;
             case 512: g.lds = Layout<512>::total; break;
             default: g.lds = Layout<1024>::total; break;
         }
@@ -2671,6 +2674,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             case 64: set_lds_limit<64>(g.lds); break;
             case 128: set_lds_limit<128>(g.lds); break;
             case 256: set_lds_limit<256>(g.lds); break;
+            case 384: set_lds_limit<384>(g.lds); break;
             case 512: set_lds_limit<512>(g.lds); break;
             case 1024: set_lds_limit<1024>(g.lds); break;
             default: set_lds_limit<0>(g.lds); break;
