@@ -1,13 +1,13 @@
-# per-phase cycle stamps (diagnostic build) for a few configurations
+# per-phase cycle stamps (diagnostic build) for the BASELINE configurations -> gpurun_out/stamps_*.json
 mkdir -p gpurun_out
-out=gpurun_out/stamps.jsonl; : > $out
-for args in "--sampled-times 1" "--sampled-times 5" "--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1" "--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5"; do
-  MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu $args >> $out 2> gpurun_out/stamps.err || exit $?
+run() { name=$1; shift; MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu "$@" > gpurun_out/stamps_$name.json 2> gpurun_out/stamps.err || exit $?; }
+run 3m_k1 --sampled-times 1
+run 3m_k5 --sampled-times 5
+run 27m_k1 --map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1
+run 27m_k5 --map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5
+run 3s5z_k5 --map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5
+for f in gpurun_out/stamps_*.json; do
+  python -c "
+import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); pc=d['roofline']['phase_cycles']
+print('$f', d['roofline']['avg_launch_us'], ' '.join(f'{k}={v:.0f}' for k,v in pc.items()))"
 done
-python - $out <<'PY'
-import json, sys
-for line in open(sys.argv[1]):
-    d = json.loads(line); r = d["roofline"]; c = d["config"]; pc = r.get("phase_cycles") or {}
-    print(c["map"], c["sampled_times"], f"{d['value']/1e6:.2f}M", r["avg_launch_us"], "path", r["mean_path_len"])
-    print("   ", " ".join(f"{k}={v:.0f}" for k, v in pc.items()))
-PY
