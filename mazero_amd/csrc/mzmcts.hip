@@ -1264,18 +1264,16 @@ __device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds
 #pragma unroll
                 for (int u = 0; u < 4; ++u) sc[u] = s.Sc[fc + ((i0 + u < nc) ? i0 + u : i0)];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
+                for (int u = 0; u < 4; ++u) {  // branch-free (selects): lanes diverge in nc
                     const int i = i0 + u;
-                    if (i < nc) {
-                        if (mx < sc[u]) {
-                            mx = sc[u];
-                            lst = 1ull << i;
-                            cnt = 1;
-                        } else if (sc[u] >= mx - 0.000001f) {
-                            lst |= 1ull << i;
-                            ++cnt;
-                        }
-                    }
+                    const float v = sc[u];
+                    const bool ok = i < nc;
+                    const bool gt = ok && (mx < v);
+                    const bool ge = ok && !gt && (v >= mx - 0.000001f);
+                    const unsigned long long bit = 1ull << (i & 63);
+                    lst = gt ? bit : (ge ? (lst | bit) : lst);
+                    cnt = gt ? 1 : (cnt + (ge ? 1 : 0));
+                    mx = gt ? v : mx;
                 }
             }
             if (cnt == 1 && !terr) {
