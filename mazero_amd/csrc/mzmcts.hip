@@ -318,6 +318,7 @@ struct Lds {
     unsigned *rng;
     float *boot;
     int2 *reg;
+    int *il;  // internal-node list of the precomputed walk (layout classes)
 };
 
 // LDS layout of k_step.  Capacity classes NC = 64 .. 1024 (node pool K*(S+2) <= NC) have a
@@ -347,7 +348,8 @@ struct Layout {
     static constexpr int oX = oReg + r16(8 * kRegCap);
     static constexpr int oPar = oX + r16(8 * (2 * MZ_S_COUNT + 4));
     static constexpr int oSc = oPar + r16(4 * NC);
-    static constexpr int total = oSc + r16(4 * NC);
+    static constexpr int oIl = oSc + r16(4 * NC);
+    static constexpr int total = oIl + r16(4 * NC);
 };
 
 template <int NC>
@@ -372,6 +374,7 @@ __device__ __forceinline__ Lds make_lds(unsigned char *m, const Geo &g) {
         s.reg = (int2 *)(m + L::oReg);
         s.Par = (int *)(m + L::oPar);
         s.Sc = (float *)(m + L::oSc);
+        s.il = (int *)(m + L::oIl);
     } else {
         s.A = (int4 *)(m + g.oA);
         s.B = (int4 *)(m + g.oB);
@@ -390,6 +393,7 @@ __device__ __forceinline__ Lds make_lds(unsigned char *m, const Geo &g) {
         s.reg = (int2 *)(m + g.oReg);
         s.Par = (int *)(m + g.oPar);
         s.Sc = (float *)(m + g.oSc);
+        s.il = nullptr;
     }
     return s;
 }
@@ -1214,30 +1218,39 @@ __device__ __forceinline__ float path_score(const Geo &g, const Lds &s, int pare
 template <int NC>
 constexpr bool kWalkPrecomputed = (NC > 0 && NC <= 384);
 
-// General trees, small pools: select_child resolved for every internal node first (scores per
-// node by value_scores, one lane per internal node for the tie lists), then a pointer chase.
-__device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base, unsigned rw0, unsigned rw1,
-                            int &err, int &out_idx, int &out_act, long long *stl, float disc, int cursor0, int wbase) {
+// The internal nodes (children count > 0) among nodes [0, tot), compacted into s.il in node
+// order with ballots; returns their number (wave-uniform).
+__device__ __forceinline__ int compact_internal(Lds &s, int tot) {
     const int l = lane_id();
-    long long scored = 0;
-#ifdef MZ_PROBE3
-    unsigned long long q0 = __builtin_amdgcn_s_memtime(), q1 = 0, q2 = 0, q3 = 0;
-#endif
-    // (1) internal nodes (children count > 0), compacted into s.boot (free once the
-    // back-propagation is done); every other node gets the walk's stop mark (s.Par: the parent
-    // indices are not needed after value_scores)
-    constexpr int kNxtLeaf = -1, kNxtSlow = -2;
-    int *ilist = (int *)s.boot;
-    int *nxt = s.Par;
     int nint = 0;
     for (int base = 0; base < tot; base += kWave) {
         const int n = base + l;
         const bool in = n < tot && nc_of(s.B[n].y) > 0;
         const unsigned long long m = ballot(in);
-        if (in) ilist[nint + __popcll(m & ((1ull << l) - 1ull))] = n;
-        else if (n < tot) nxt[n] = kNxtLeaf;
+        if (in) s.il[nint + __popcll(m & ((1ull << l) - 1ull))] = n;
         nint += __popcll(m);
     }
+    wait_lds();
+    return uni(nint);
+}
+
+// General trees, small pools: select_child resolved for every internal node first (scores per
+// node by value_scores, one lane per internal node for the tie lists), then a pointer chase.
+__device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base, unsigned rw0, unsigned rw1,
+                            int &err, int &out_idx, int &out_act, long long *stl, float disc, int cursor0, int wbase,
+                            int nint_pre) {
+    const int l = lane_id();
+    long long scored = 0;
+#ifdef MZ_PROBE3
+    unsigned long long q0 = __builtin_amdgcn_s_memtime(), q1 = 0, q2 = 0, q3 = 0;
+#endif
+    // (1) internal nodes (children count > 0) in s.il: compacted by the expanding wave while it
+    // waited for the back-propagation (nint_pre >= 0), else here
+    constexpr int kNxtLeaf = -1, kNxtSlow = -2;
+    int *ilist = s.il;
+    int *nxt = s.Par;  // (the parent indices are not needed after value_scores)
+    int nint = nint_pre;
+    if (nint < 0) nint = compact_internal(s, tot);
     wait_lds();
 #ifdef MZ_PROBE3
     q1 = __builtin_amdgcn_s_memtime();
@@ -1300,7 +1313,9 @@ __device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds
         const int rv = uni(s.A[0].x);
         const int nc0 = nc_of(r0b.y);
         int v;
-        if (nc0 > 0 && rv <= nc0) {
+        if (nc0 == 0) {
+            v = kNxtLeaf;
+        } else if (rv <= nc0) {
             v = r0b.x + rv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
         } else {
             v = uni(nxt[0]);
@@ -1342,7 +1357,9 @@ __device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds
             ++D;
             if (D < kWave) px = wl(px, x, D);
             else if (l == 0) s.path[D].x = x;
-            v = uni(nxt[x]);
+            const int vn = nxt[x];
+            const int ncx = uni(nc_of(s.B[x].y));
+            v = (ncx == 0) ? kNxtLeaf : uni(vn);  // (nxt holds records of internal nodes only)
             if (v >= 0) ++cursor;
         }
     }
@@ -1535,7 +1552,7 @@ __device__ __forceinline__ void walk_levels(const Geo &g, const Dev &d, Lds &s, 
 template <int NC>
 __device__ __forceinline__ void select_walk(const Geo &g, const Dev &d, Lds &s, int t, int tot, TreeHdr &h, int lds_base,
                             unsigned rw0, unsigned rw1, int &err, int &out_idx, int &out_act, long long *stl,
-                            bool fast, float disc) {
+                            bool fast, float disc, int nint_pre) {
     const int l = lane_id();
     const int cursor0 = h.cursor;
     const int wbase = cursor0;  // register window [wbase, wbase + 128)
@@ -1587,7 +1604,8 @@ __device__ __forceinline__ void select_walk(const Geo &g, const Dev &d, Lds &s, 
     }
 
     if constexpr (kWalkPrecomputed<NC>)
-        walk_precomputed(g, d, s, t, tot, h, lds_base, rw0, rw1, err, out_idx, out_act, stl, disc, cursor0, wbase);
+        walk_precomputed(g, d, s, t, tot, h, lds_base, rw0, rw1, err, out_idx, out_act, stl, disc, cursor0, wbase,
+                         nint_pre);
     else
         walk_levels(g, d, s, t, tot, h, lds_base, rw0, rw1, err, out_idx, out_act, stl, disc, cursor0, wbase);
 }
@@ -1914,6 +1932,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
 
     int cursor = h.cursor;
     int ntot = tot;
+    int nint_pre = -1;  // internal nodes compacted early by wave 0 (precomputed walk)
     if (EB) {
         if (wv == 0) {
             // ---- CTree::expand (cnode.cpp:224-295) of the leaf (expand_and_backprop, :452-469) ----
@@ -1940,6 +1959,15 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
                 const int4 nbv = make_int4(tot, pack_y(nc, act_of(ly), md), f2i(v_in), a.hsx);
                 s.B[leaf] = nbv;
                 d.Bn()[nb + leaf] = nbv;
+            }
+            if constexpr (SEL && !JOINT && kWalkPrecomputed<NC>) {
+                // while the other wave back-propagates: the selection's internal-node list (children
+                // counts do not change in the back-propagation; this simulation's new children are
+                // leaves, so nodes [0, tot) with the leaf's record just written)
+                if (g.K > 1 && !err) {
+                    wait_lds();
+                    nint_pre = compact_internal(s, tot);
+                }
             }
             stamp(ts, 4);
         } else {
@@ -2021,7 +2049,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         asm volatile("" ::"v"(rw0), "v"(rw1));
         stl[MZ_S_CYC_EXP_DRAW] = (long long)(__builtin_amdgcn_s_memtime() - v0);  // up to the walk
 #endif
-        select_walk<NC>(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast, a.discount);
+        select_walk<NC>(g, d, s, t, h.tot, h, wbase, rw0, rw1, err, idx, act, stl, fast, a.discount, nint_pre);
         if (l == 0) {
             a.idx_x[t] = idx;
             a.idy[t] = t;
