@@ -323,7 +323,8 @@ def pmc_traffic(args):
 
 
 def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):
-    """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs."""
+    """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs;
+    plus the same on up to 16 host cores at once ("multi_core", informational)."""
     from mazero_amd import _capi
     from mazero_amd.cytree import Tree_batch
     from mazero_amd.synthetic import DEFAULTS
@@ -356,6 +357,43 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):
             tree_time += time.perf_counter() - t0
             sims += B * S
         steps += 1
+    # (ii) SURVEY §8(d): the same searches on several host cores at once -- independent tree
+    # batches, one per thread (the reference ctree releases the GIL inside its ctypes calls), as
+    # many threads as this process's CPU share allows, at most 16 (the GPU box's share per GPU)
+    def worker(budget, out, k):
+        n_sims, t_run, t0w = 0, 0.0, time.perf_counter()
+        while time.perf_counter() - t0w < budget:
+            for inp in host_inputs:
+                tb = Tree_batch(B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"], lib=lib)
+                ts = time.perf_counter()
+                tb.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps,
+                           inp.root_noise)
+                for s in range(S):
+                    tb.batch_selection(c2, c1, g)
+                    tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s],
+                                                  inp.beta[s])
+                tb.get_roots_values()
+                tb.get_roots_marginal_visit_count()
+                t_run += time.perf_counter() - ts
+                n_sims += B * S
+        out[k] = (n_sims, t_run)
+
+    import threading
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    n_thr = max(1, min(16, share))
+    res = [None] * n_thr
+    t0 = time.perf_counter()
+    thr = [threading.Thread(target=worker, args=(budget_s / 2, res, k)) for k in range(n_thr)]
+    for x in thr:
+        x.start()
+    for x in thr:
+        x.join()
+    wall = time.perf_counter() - t0
+    multi = {"value": round(sum(r[0] for r in res) / wall, 1), "threads": n_thr,
+             "sample": f"{sum(r[0] for r in res)} sims in {wall:.1f} s wall, one independent tree batch per thread"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -372,6 +410,7 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):
         "kind": kind,
         "sample": f"{steps} env steps x {N} searches x {B} roots x {S} sims (K={K}) = {sims} sims, "
                   f"{tree_time:.1f} s of tree calls on 1 core of '{cpu_model}' (nproc {os.cpu_count()})",
+        "multi_core": multi,
     }
 
 
