@@ -7,5 +7,5 @@ for args in "--sampled-times 1" "--sampled-times 5" "--map 27m_vs_30m --roots 25
   MZ_LIB_OVERRIDE=$lib timeout -k 10 200 python bench.py --no-cpu $args > gpurun_out/ab1.json 2>> gpurun_out/ab.err || exit $?
   python -c "
 import json; d=json.loads(open('gpurun_out/ab1.json').read().strip().splitlines()[-1]); c=d['config']
-print('$lib'.split('/')[-1], c['map'], 'K=%d' % c['sampled_times'], d['roofline']['avg_launch_us'])"
+print('$lib'.split('/')[-1], c['map'], 'K=%d' % c['sampled_times'], d['roofline']['avg_launch_us'], round(d['value']/1e6, 2))"
 done; done; done
