@@ -13,20 +13,26 @@ policy = beta, reward 0.1*N(0,1), value N(0,1), Dirichlet(0.3) root noise, hidde
 [51, 256, 3*128] fp32 that the fused kernel gathers from).  The whole step (3 searches) is
 captured once in a HIP graph and replayed.
 
-Multi-GPU (torchrun, one process per GPU): roots are independent (cnode.cpp:633-641), so every
-rank searches its own 256 roots (global root offset rank*256, seeds random_seed*2333+global index)
-with no collective on the data path -> "scaling": "weak".  The barrier / max-over-ranks timing uses
-torch.distributed (RCCL).
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every process is one rank;
+`python bench.py --gpus N` without torchrun starts the N ranks itself (torch.distributed.run, before
+anything touches the GPU) and n_gpus is the job's world size.  Roots are independent
+(cnode.cpp:633-641), so ranks share no data-path collective:
+  weak   (headline, "scaling": "weak")  every rank searches its own --roots roots (global root
+         offset rank*roots, tree seeds random_seed*2333 + global index);
+  strong (N > 1, reported beside it as "strong_scaling")  the --roots roots split over the ranks.
+`--strong` swaps the two.  The barrier / max-over-ranks clock uses torch.distributed (RCCL).
 
 Also reported (rank 0, N=1 only):
   roofline      dominant kernel k_step<true,true> (fused simulation step): algorithmic bytes per
                 launch (SURVEY §8d formula over the kernel's own counters) / its average duration,
                 measured with HIP events on the launch stream around a graph of one search's 49
                 back-to-back fused launches; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per launch
-                from profiles/pmc_latest.json (scripts/pmc_summary.py) for the same workload
+                from profiles/pmc_latest.json (scripts/pmc_summary.py) for the same workload,
+                2 x FETCH_SIZE + WRITE_SIZE (the guide's gfx950 correction; raw beside it)
   cpu_baseline  the reference C++ ctree (oracle/_ref/libmzref.so, compiled from the reference
                 sources) -- or the CPU port when that is absent -- on the same synthetic inputs,
-                one host core, timing only the tree calls, over a bounded sample (~10 s)
+                one host core, timing only the tree calls, over a bounded sample (~10 s); plus
+                "multi_core": one process per host core (up to --cpu-procs), roots sharded
 """
 from __future__ import annotations
 
@@ -53,156 +59,153 @@ CONFIGS = {  # name: (agents N, actions A) -- smac_maps.py:17-133, n_actions = 6
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU); without torchrun's WORLD_SIZE, N > 1 spawns them")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--map", default="3m", choices=sorted(CONFIGS))
-    ap.add_argument("--roots", type=int, default=256, help="roots per GPU")
+    ap.add_argument("--roots", type=int, default=256, help="roots per GPU (weak scaling) / in total (strong)")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--sampled-times", type=int, default=1, help="K (core/config.py:86 default 1)")
-    ap.add_argument("--strong", action="store_true", help="split --roots over the GPUs instead of per GPU")
+    ap.add_argument("--strong", action="store_true",
+                    help="headline value from the strong-scaling leg (--roots split over the GPUs)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="processes of the multi-core CPU baseline (at most this process's CPU share)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--backend", default="hip", choices=("hip", "port"),
+                    help="'port': every rank searches on the host with the CPU port over gloo -- a CPU "
+                         "test of the launcher / sharding / clock plumbing only, never a measurement")
     return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def launch(args) -> int:
+    """`--gpus N` without torchrun: start N ranks under torch.distributed.run (one process per GPU)
+    and return its exit status.  Nothing here touches the GPU, so the ranks start clean."""
+    import socket
+    import subprocess
 
-    from mazero_amd._lib import load
-    from mazero_amd.cytree import Tree_batch
-    from mazero_amd.synthetic import DEFAULTS, HIDDEN_PER_AGENT, make_search_inputs
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=dict(os.environ))
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
-    lib = load()
 
-    N, A = CONFIGS[args.map]
-    S, K = args.sims, args.sampled_times
-    B = args.roots // world if args.strong else args.roots
-    root_offset = rank * B
-    H = N * HIDDEN_PER_AGENT
-    d = DEFAULTS
-    c2, c1, g = d["pb_c_base"], d["pb_c_init"], d["discount"]
+class HipLeg:
+    """One rank's searches on its GPU: N sequential agent searches over B roots (global root
+    offset `root_offset`), inputs and network outputs resident in HBM, the whole env step captured
+    in one HIP graph."""
 
-    # ---- synthetic inputs, one set per agent search, resident in HBM ----
-    rng = np.random.default_rng(args.seed * 1000 + rank)
-    host_inputs = [make_search_inputs(rng, B, A, S) for _ in range(N)]
+    def __init__(self, args, B, root_offset, rank, lib, dev, stream):
+        import torch
 
-    def dev_t(a):
-        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        from mazero_amd.cytree import Tree_batch
+        from mazero_amd.synthetic import DEFAULTS, HIDDEN_PER_AGENT, make_search_inputs
 
-    searches = []
-    for inp in host_inputs:
-        tb = Tree_batch(B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"], root_offset=root_offset, lib=lib)
-        # one allocation per search for the network outputs ([S, B | B | B*A | B*A]) and one for
-        # the selection outputs: every distinct allocation a kernel touches costs a translation miss
-        net = dev_t(np.concatenate([inp.reward.reshape(S, -1), inp.value.reshape(S, -1), inp.policy.reshape(S, -1),
-                                    inp.beta.reshape(S, -1)], axis=1))
-        sel = torch.empty(3, B, dtype=torch.int32, device=dev)
-        searches.append(dict(
-            tb=tb,
-            rr=dev_t(inp.root_reward), rv=dev_t(inp.root_value), rp=dev_t(inp.root_policy),
-            rb=dev_t(inp.root_beta), rn=dev_t(inp.root_noise), eps=inp.noise_eps,
-            r=net[:, :B], v=net[:, B:2 * B], p=net[:, 2 * B:2 * B + B * A], b=net[:, 2 * B + B * A:],
-            pool=torch.randn(S + 1, B, H, device=dev),
-            leaf=torch.empty(B, H, device=dev),
-            idx=sel[0], idy=sel[1], act=sel[2].view(B, 1),
-            values=torch.empty(B, device=dev),
-            visits=torch.empty(B, 1, A, dtype=torch.int32, device=dev),
-        ))
+        self.args, self.B, self.lib, self.stream = args, B, lib, stream
+        N, A = CONFIGS[args.map]
+        S, K = args.sims, args.sampled_times
+        self.N, self.A, self.S, self.K, self.H = N, A, S, K, N * HIDDEN_PER_AGENT
+        d = DEFAULTS
+        self.c2, self.c1, self.g = d["pb_c_base"], d["pb_c_init"], d["discount"]
+        # synthetic inputs, one set per agent search, drawn for the global root range of this rank
+        rng = np.random.default_rng(args.seed * 1000 + rank)
+        self.host_inputs = [make_search_inputs(rng, B, A, S) for _ in range(N)]
 
-    fused_events = []
+        def dev_t(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
-    def one_search(sd, timed_events=None):
+        self.searches = []
+        for inp in self.host_inputs:
+            tb = Tree_batch(B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"], root_offset=root_offset,
+                            lib=lib)
+            # one allocation per search for the network outputs ([S, B | B | B*A | B*A]) and one for
+            # the selection outputs: every distinct allocation a kernel touches costs a translation miss
+            net = dev_t(np.concatenate([inp.reward.reshape(S, -1), inp.value.reshape(S, -1),
+                                        inp.policy.reshape(S, -1), inp.beta.reshape(S, -1)], axis=1))
+            sel = torch.empty(3, B, dtype=torch.int32, device=dev)
+            self.searches.append(dict(
+                tb=tb,
+                rr=dev_t(inp.root_reward), rv=dev_t(inp.root_value), rp=dev_t(inp.root_policy),
+                rb=dev_t(inp.root_beta), rn=dev_t(inp.root_noise), eps=inp.noise_eps,
+                r=net[:, :B], v=net[:, B:2 * B], p=net[:, 2 * B:2 * B + B * A], b=net[:, 2 * B + B * A:],
+                pool=torch.randn(S + 1, B, self.H, device=dev),
+                leaf=torch.empty(B, self.H, device=dev),
+                idx=sel[0], idy=sel[1], act=sel[2].view(B, 1),
+                values=torch.empty(B, device=dev),
+                visits=torch.empty(B, 1, A, dtype=torch.int32, device=dev),
+            ))
+        self.graph = None
+
+    def one_search(self, sd):
+        S, K, c2, c1, g = self.S, self.K, self.c2, self.c1, self.g
         tb = sd["tb"]
         out = (sd["idx"], sd["idy"], sd["act"])
         tb.prepare(sd["rr"], sd["rv"], sd["rp"], sd["rb"], K, sd["eps"], sd["rn"])
         tb.batch_selection_device(c2, c1, g, out=out)
         for s in range(S):
             if s + 1 < S:
-                if timed_events is not None:
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
                 tb.expansion_backup_selection_device(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s],
                                                      c2, c1, out=out, pool=sd["pool"], gather_out=sd["leaf"])
-                if timed_events is not None:
-                    e1.record()
-                    timed_events.append((e0, e1))
             else:
                 tb.batch_expansion_and_backup(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s])
         # search outputs stay on the device (mcts_sampled.py:176-191)
-        lib.mz_get_roots_values(tb._h, C.c_void_p(sd["values"].data_ptr()), 1)
-        lib.mz_get_roots_marginal_visit_count(tb._h, C.c_void_p(sd["visits"].data_ptr()), 1)
+        self.lib.mz_get_roots_values(tb._h, C.c_void_p(sd["values"].data_ptr()), 1)
+        self.lib.mz_get_roots_marginal_visit_count(tb._h, C.c_void_p(sd["visits"].data_ptr()), 1)
 
-    def env_step():
-        for sd in searches:  # agents searched sequentially (selfplay_worker.py:196-211)
-            one_search(sd)
+    def env_step(self):
+        for sd in self.searches:  # agents searched sequentially (selfplay_worker.py:196-211)
+            self.one_search(sd)
 
-    # warm-up (also builds the pUCT tables, so nothing host->device happens inside the graph)
-    stream = torch.cuda.Stream()
-    torch.cuda.synchronize()
-    with torch.cuda.stream(stream):
-        for _ in range(max(1, args.warmup)):
-            env_step()
-    torch.cuda.synchronize()
+    def prepare(self):
+        """Warm-up (also builds the pUCT tables, so nothing host->device happens inside the graph),
+        then the graph of one env step."""
+        import torch
 
-    graph = None
-    if not args.no_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=stream):
-            env_step()
         torch.cuda.synchronize()
-        for _ in range(max(1, args.warmup)):
-            graph.replay()
+        with torch.cuda.stream(self.stream):
+            for _ in range(max(1, self.args.warmup)):
+                self.env_step()
         torch.cuda.synchronize()
-    for sd in searches:
-        sd["tb"].synchronize()  # surfaces any deferred device-side error before timing
-    stats0 = [sd["tb"].stats() for sd in searches]
+        if not self.args.no_graph:
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=self.stream):
+                self.env_step()
+            torch.cuda.synchronize()
+            for _ in range(max(1, self.args.warmup)):
+                self.graph.replay()
+            torch.cuda.synchronize()
+        self.check()
 
-    # ---- timed region ----
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        for _ in range(args.steps):
-            if graph is not None:
-                graph.replay()
-            else:
-                env_step()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    for sd in searches:
-        sd["tb"].synchronize()
-    stats1 = [sd["tb"].stats() for sd in searches]
+    def check(self):
+        for sd in self.searches:
+            sd["tb"].synchronize()  # surfaces any deferred device-side error
 
-    sims_per_rank = B * S * N * args.steps
-    value = sims_per_rank * world / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
+    def stats(self):
+        return [sd["tb"].stats() for sd in self.searches]
 
-    # ---- roofline of the dominant kernel (rank 0) ----
-    roofline = None
-    if rank == 0:
+    def run(self, steps):
+        import torch
+
+        with torch.cuda.stream(self.stream):
+            for _ in range(steps):
+                if self.graph is not None:
+                    self.graph.replay()
+                else:
+                    self.env_step()
+
+    def roofline(self, stats0, stats1, steps):
+        """Algorithmic bytes per launch of the fused kernel over its measured average duration."""
+        import torch
+
+        N, A, K, S, B, H = self.N, self.A, self.K, self.S, self.B, self.H
+        c2, c1, g = self.c2, self.c1, self.g
         st = {k: sum(s1[k] - s0[k] for s0, s1 in zip(stats0, stats1)) for k in stats1[0]}
-        launches_fused = N * (S - 1) * args.steps
+        launches_fused = N * (S - 1) * steps
         # SURVEY.md §8(d) per-simulation algorithmic bytes, over the kernel's own counters
         sel_b = 20 * st["path_edges"] + 20 * st["scored"] + 16 * st["selects"]
         exp_b = st["expands"] * (8 * A + 8 * K + 12) + 40 * st["new_children"]
@@ -211,25 +214,24 @@ def main():
         # the fused kernel does all of it except the prepare-time expansion and the first selection
         # and the last (non-fused) expansion of each search: attribute proportionally
         frac_fused = (S - 1) / (S + 1)
-        bytes_fused = (sel_b + exp_b + bak_b) * frac_fused + gat_b
-        bytes_per_launch = bytes_fused / launches_fused
+        bytes_per_launch = ((sel_b + exp_b + bak_b) * frac_fused + gat_b) / launches_fused
         # Average duration of the fused kernel, measured with HIP events on the launch stream: a
         # graph holding one search's S-1 fused launches (back to back, as in the timed region) is
         # replayed after an eager prepare + first selection; (e1 - e0) / (S - 1) per replay.
-        sd0 = searches[0]
+        sd0 = self.searches[0]
         tb0 = sd0["tb"]
         out0 = (sd0["idx"], sd0["idy"], sd0["act"])
         steps_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(stream):
+        with torch.cuda.stream(self.stream):
             tb0.prepare(sd0["rr"], sd0["rv"], sd0["rp"], sd0["rb"], K, sd0["eps"], sd0["rn"])
             tb0.batch_selection_device(c2, c1, g, out=out0)
         torch.cuda.synchronize()
-        with torch.cuda.graph(steps_graph, stream=stream):
+        with torch.cuda.graph(steps_graph, stream=self.stream):
             for s in range(S - 1):
                 tb0.expansion_backup_selection_device(s + 1, g, K, sd0["r"][s], sd0["v"][s], sd0["p"][s], sd0["b"][s],
                                                       c2, c1, out=out0, pool=sd0["pool"], gather_out=sd0["leaf"])
         durs = []
-        with torch.cuda.stream(stream):
+        with torch.cuda.stream(self.stream):
             for rep in range(6):
                 tb0.prepare(sd0["rr"], sd0["rv"], sd0["rp"], sd0["rb"], K, sd0["eps"], sd0["rn"])
                 tb0.batch_selection_device(c2, c1, g, out=out0)
@@ -245,27 +247,176 @@ def main():
         tb0.synchronize()
         avg = float(np.median(durs))
         achieved = bytes_per_launch / avg / 1e9
-        roofline = dict(
+        pmc = pmc_traffic(self.args)
+        r = dict(
             kernel="k_step<true,true> (fused expand+backup+select+gather)",
             bound="hbm",
             achieved=round(achieved, 3),
             peak=8000.0,
             unit="GB/s",
             frac=round(achieved / 8000.0, 6),
-            traffic=pmc_traffic(args),
+            traffic=None if pmc is None else pmc.get("fused_bytes_per_launch_corrected"),
+            traffic_raw=None if pmc is None else pmc.get("fused_bytes_per_launch"),
+            traffic_note="rocprofv3 PMC, bytes per fused launch: 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md "
+                         "§HBM gfx950 correction); traffic_raw = FETCH_SIZE + WRITE_SIZE",
             bytes_per_launch=round(bytes_per_launch, 1),
             avg_launch_us=round(avg * 1e6, 3),
             mean_path_len=round(st["path_edges"] / max(1, st["selects"]), 3),
         )
         if os.environ.get("MZ_STAMPS") == "1" and st.get("stamped", 0) > 0:
             # diagnostic build: average shader cycles per fused launch and tree, per phase
-            roofline["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
+            r["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
+        return r
 
+
+class PortLeg:
+    """--backend port (CPU test of the multi-rank plumbing only): the same searches of this rank's
+    roots on the host with the CPU port library."""
+
+    def __init__(self, args, B, root_offset, rank):
+        from mazero_amd import _capi
+        from mazero_amd.synthetic import DEFAULTS, make_search_inputs
+
+        path = os.path.join(ROOT, "oracle", "_build", "libmzport.so")
+        self.lib = _capi.bind(C.CDLL(path))
+        self.args, self.B, self.root_offset = args, B, root_offset
+        N, A = CONFIGS[args.map]
+        self.N, self.A, self.S, self.K = N, A, args.sims, args.sampled_times
+        self.d = DEFAULTS
+        rng = np.random.default_rng(args.seed * 1000 + rank)
+        self.host_inputs = [make_search_inputs(rng, B, A, self.S) for _ in range(N)]
+        self.graph = None
+        self.values = None
+
+    def env_step(self):
+        from mazero_amd.cytree import Tree_batch
+        from mazero_amd.synthetic import run_search
+
+        d, out = self.d, []
+        for inp in self.host_inputs:
+            tb = Tree_batch(self.B, 1, self.A, self.K, self.S, d["delta_lb"], inp.seed, d["rho"], d["lam"],
+                            root_offset=self.root_offset, lib=self.lib)
+            run_search(tb, inp, self.K, record=False)
+            out.append(tb.get_roots_values())
+        self.values = out
+
+    def prepare(self):
+        self.env_step()
+
+    def check(self):
+        pass
+
+    def run(self, steps):
+        for _ in range(steps):
+            self.env_step()
+
+
+def timed(leg, steps, world, dist, sync, dev):
+    """EXACTLY `steps` env steps between barrier + device synchronisation on both sides; the max
+    over ranks of the wall time."""
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    leg.run(steps)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+
+        dist.barrier()
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    leg.check()
+    return elapsed
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
+    import torch
+    import torch.distributed as dist
+
+    from mazero_amd.shard import shard_bounds
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    hip = args.backend == "hip"
+    if hip:
+        torch.cuda.set_device(local if world > 1 else 0)
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        if hip:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        world = dist.get_world_size()
+        rank = dist.get_rank()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)")
+    sync = torch.cuda.synchronize if hip else (lambda: None)
+    N, A = CONFIGS[args.map]
+    S, K = args.sims, args.sampled_times
+
+    if hip:
+        from mazero_amd._lib import load
+
+        lib = load()
+        stream = torch.cuda.Stream()
+
+        def make_leg(B, off):
+            return HipLeg(args, B, off, rank, lib, dev, stream)
+    else:
+        def make_leg(B, off):
+            return PortLeg(args, B, off, rank)
+
+    # weak scaling: every rank owns --roots roots (global root offset rank * roots)
+    # strong scaling: --roots split over the ranks (only measured separately when world > 1)
+    legs = {}
+    order = ["strong", "weak"] if args.strong else ["weak", "strong"]
+    if world == 1:
+        order = order[:1]
+    for kind in order:
+        if kind == "weak":
+            B, off, total = args.roots, rank * args.roots, args.roots * world
+        else:
+            lo, hi = shard_bounds(args.roots, world, rank)
+            B, off, total = hi - lo, lo, args.roots
+        leg = make_leg(B, off)
+        leg.prepare()
+        st0 = leg.stats() if hip and rank == 0 else None
+        elapsed = timed(leg, args.steps, world, dist, sync, dev)
+        st1 = leg.stats() if hip and rank == 0 else None
+        legs[kind] = dict(leg=leg, B=B, total=total, elapsed=elapsed, st0=st0, st1=st1)
+
+    main_kind = order[0]
+    m = legs[main_kind]
+    value = m["total"] * S * N * args.steps / m["elapsed"]
+    roofline = None
+    if hip and rank == 0:
+        roofline = m["leg"].roofline(m["st0"], m["st1"], args.steps)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(host_inputs, B, A, K, S, N, args.cpu_seconds)
+    if hip and rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(m["leg"].host_inputs, m["B"], A, K, S, N, args.cpu_seconds, args.cpu_procs)
 
     if rank == 0:
+        other = {}
+        for kind, lg in legs.items():
+            if kind == main_kind:
+                continue
+            other[f"{kind}_scaling"] = dict(
+                value=round(lg["total"] * S * N * args.steps / lg["elapsed"], 1),
+                unit="simulations/s",
+                ms_per_step=round(lg["elapsed"] / args.steps * 1e3, 4),
+                roots_total=lg["total"],
+                roots_per_gpu=lg["B"],
+                steps=args.steps,
+            )
         line = {
             "metric": "MCTS simulations/sec (whole node), SMAC 3m, 256 roots×50 sims, 1/2/4/8 GPUs"
             if args.map == "3m" else f"MCTS simulations/sec (whole node), SMAC {args.map}",
@@ -274,30 +425,35 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": round(m["elapsed"] / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": main_kind,
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (device-resident network outputs + hidden-state pool, SURVEY §8d)",
+            "data": "synthetic (device-resident network outputs + hidden-state pool, SURVEY §8d)" if hip
+            else "synthetic; --backend port: CPU port on every rank (plumbing test, not a measurement)",
             "config": {
-                "workload": f"SMAC {args.map} self-play search: {N} sequential agent searches x {B} roots/GPU x {S} sims",
+                "workload": f"SMAC {args.map} self-play search: {N} sequential agent searches x {m['B']} roots/GPU "
+                            f"x {S} sims",
                 "map": args.map,
                 "agents": N,
                 "actions": A,
-                "roots_per_gpu": B,
-                "roots_total": B * world,
+                "roots_per_gpu": m["B"],
+                "roots_total": m["total"],
                 "sims": S,
                 "sampled_times": K,
-                "hidden": H,
-                "graph": graph is not None,
+                "hidden": N * 128,
+                "graph": hip and not args.no_graph,
+                "backend": args.backend,
                 "parallelism": f"roots sharded over {world} GPU(s), no collective on the data path",
             },
+            **other,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 
@@ -315,18 +471,46 @@ def pmc_traffic(args):
             pm = json.load(f)
     except (OSError, ValueError):
         return None
-    key = workload_key(args)
-    ent = pm.get("workloads", {}).get(key)
-    if not ent:
-        return None
-    return ent.get("fused_bytes_per_launch")
+    return pm.get("workloads", {}).get(workload_key(args)) or None
 
 
-def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):
-    """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs;
-    plus the same on up to 16 host cores at once ("multi_core", informational)."""
+def _cpu_worker(path, shards, B, A, K, S, budget_s, start, q):
+    """One host process of the multi-core CPU baseline: this process's root shard of every agent
+    search, searched with the CPU tree library until the budget is spent (tree calls only)."""
     from mazero_amd import _capi
     from mazero_amd.cytree import Tree_batch
+    from mazero_amd.synthetic import DEFAULTS
+
+    lib = _capi.bind(C.CDLL(path))
+    d = DEFAULTS
+    c2, c1, g = d["pb_c_base"], d["pb_c_init"], d["discount"]
+    start.wait()
+    n_sims, t_run, t0 = 0, 0.0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        for inp in shards:
+            tb = Tree_batch(inp.B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"], lib=lib)
+            ts = time.perf_counter()
+            tb.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps,
+                       inp.root_noise)
+            for s in range(S):
+                tb.batch_selection(c2, c1, g)
+                tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+            tb.get_roots_values()
+            tb.get_roots_marginal_visit_count()
+            t_run += time.perf_counter() - ts
+            n_sims += inp.B * S
+    q.put((n_sims, t_run, time.perf_counter() - t0))
+
+
+def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16):
+    """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs; plus
+    SURVEY §8(d)(ii): the same env steps on several host cores at once, one process per core with
+    the roots sharded over the processes ("multi_core")."""
+    import multiprocessing as mp
+
+    from mazero_amd import _capi
+    from mazero_amd.cytree import Tree_batch
+    from mazero_amd.shard import shard_bounds, slice_inputs
     from mazero_amd.synthetic import DEFAULTS
 
     ref = os.path.join(ROOT, "oracle", "_ref", "libmzref.so")
@@ -357,43 +541,32 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):
             tree_time += time.perf_counter() - t0
             sims += B * S
         steps += 1
-    # (ii) SURVEY §8(d): the same searches on several host cores at once -- independent tree
-    # batches, one per thread (the reference ctree releases the GIL inside its ctypes calls), as
-    # many threads as this process's CPU share allows, at most 16 (the GPU box's share per GPU)
-    def worker(budget, out, k):
-        n_sims, t_run, t0w = 0, 0.0, time.perf_counter()
-        while time.perf_counter() - t0w < budget:
-            for inp in host_inputs:
-                tb = Tree_batch(B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"], lib=lib)
-                ts = time.perf_counter()
-                tb.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps,
-                           inp.root_noise)
-                for s in range(S):
-                    tb.batch_selection(c2, c1, g)
-                    tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s],
-                                                  inp.beta[s])
-                tb.get_roots_values()
-                tb.get_roots_marginal_visit_count()
-                t_run += time.perf_counter() - ts
-                n_sims += B * S
-        out[k] = (n_sims, t_run)
-
-    import threading
+    # (ii) one process per core, the roots of every search sharded over the processes (each
+    # process's trees are seeded locally: the work per tree is the same as in the sharded batch)
     try:
-        share = len(os.sched_getaffinity(0))
+        share = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        share = os.cpu_count() or 1
-    n_thr = max(1, min(16, share))
-    res = [None] * n_thr
-    t0 = time.perf_counter()
-    thr = [threading.Thread(target=worker, args=(budget_s / 2, res, k)) for k in range(n_thr)]
-    for x in thr:
-        x.start()
-    for x in thr:
-        x.join()
-    wall = time.perf_counter() - t0
-    multi = {"value": round(sum(r[0] for r in res) / wall, 1), "threads": n_thr,
-             "sample": f"{sum(r[0] for r in res)} sims in {wall:.1f} s wall, one independent tree batch per thread"}
+        share = list(range(os.cpu_count() or 1))
+    n_proc = max(1, min(procs, len(share), B))
+    ctx = mp.get_context("spawn")  # a fresh interpreter per worker (this process may hold the GPU)
+    start, q = ctx.Event(), ctx.Queue()
+    workers = []
+    for k in range(n_proc):
+        lo, hi = shard_bounds(B, n_proc, k)
+        shards = [slice_inputs(inp, lo, hi) for inp in host_inputs]
+        w = ctx.Process(target=_cpu_worker, args=(path, shards, B, A, K, S, budget_s / 2, start, q), daemon=True)
+        w.start()
+        workers.append(w)
+    time.sleep(0.5)
+    start.set()
+    res = [q.get(timeout=budget_s * 4 + 60) for _ in workers]
+    for w in workers:
+        w.join(timeout=30)
+    wall = max(r[2] for r in res)
+    total = sum(r[0] for r in res)
+    multi = {"value": round(total / wall, 1), "processes": n_proc, "cores": n_proc,
+             "sample": f"{total} sims in {wall:.1f} s wall: {n_proc} processes, each searching its shard of "
+                       f"the {B} roots of every agent search ({kind} ctree)"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -408,8 +581,10 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s):
         "unit": "simulations/s",
         "cores": 1,
         "kind": kind,
+        "cpu_model": cpu_model,
         "sample": f"{steps} env steps x {N} searches x {B} roots x {S} sims (K={K}) = {sims} sims, "
-                  f"{tree_time:.1f} s of tree calls on 1 core of '{cpu_model}' (nproc {os.cpu_count()})",
+                  f"{tree_time:.1f} s of tree calls on 1 core of '{cpu_model}' (nproc {os.cpu_count()}, "
+                  f"this process's share {len(share)})",
         "multi_core": multi,
     }
 

@@ -118,7 +118,9 @@ int mz_create(int root_num, int agent_num, int action_space_size, int sampled_ti
               float rho, float lam, int root_offset, mz_batch **out);
 /* Replaces CTree_batch::~CTree_batch (cnode.cpp:579-587). */
 int mz_destroy(mz_batch *b);
-/* Make subsequent device work of this handle run on `stream` (a hipStream_t; NULL = default). */
+/* Make subsequent device work of this handle run on `stream` (a hipStream_t; NULL = default).
+ * Work already queued on the previous stream is ordered before it (an event wait), unless either
+ * stream is capturing a graph. */
 int mz_set_stream(mz_batch *b, void *stream);
 /* Wait for all work of this handle and report any deferred device-side error. */
 int mz_synchronize(mz_batch *b);

@@ -7,6 +7,4 @@ include/mzmcts.h.  Python surfaces:
   mazero_amd.cytree.Tree_batch        drop-in for core.mcts.ctree.ctree_sampled.cytree.Tree_batch
   mazero_amd.mcts_sampled.SampledMCTS drop-in for core.mcts.tree_search.SampledMCTS (device loop)
 """
-from . import _hipenv  # noqa: F401  (HIP runtime settings, before the runtime initialises)
-
 __all__ = ["cytree"]

@@ -183,6 +183,57 @@ __host__ __device__ __forceinline__ void arena_hot(Dev &d, long long B, long lon
     d.o_path = (unsigned)o;
 }
 
+#ifdef MZ_ARGCHECK
+// Diagnostic build (graph-replay investigation): records of inconsistent launches in a device
+// buffer, read back with mz_debug_dump (device printf does not reach the host from graph replays).
+constexpr int kDbgRecs = 64, kDbgWords = 32;
+__device__ unsigned g_dbg[kDbgRecs][kDbgWords];
+__device__ int g_dbg_n;
+__device__ unsigned g_dbg_sites;
+__device__ __noinline__ void argcheck_record(unsigned kind, bool EB, bool SEL, int t, char *base, int P, int PS,
+                                             int BA, int pk, int K, int hsx, float discount, int pe, int ne,
+                                             TreeHdr *hv, int tot, int cur, int D, int herr, const unsigned *ka,
+                                             const float *reward, const float *value, const char *pool, int err) {
+    const int gK = (int)((unsigned)pk >> 17), B = BA & 0xffffff;
+    const int tot2 = __hip_atomic_load(&hv->tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int cur2 = __hip_atomic_load(&hv->cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int D2 = __hip_atomic_load(&hv->D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    Params *pv = (Params *)base;
+    const int pP = __hip_atomic_load(&pv->g.P, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int pPS = __hip_atomic_load(&pv->g.PS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int pB = __hip_atomic_load(&pv->g.B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int pK = __hip_atomic_load(&pv->g.K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long kbase = (unsigned long long)ka[0] | ((unsigned long long)ka[1] << 32);
+    unsigned bad = 0;
+    if (tot2 != tot || cur2 != cur || D2 != D) bad |= 1;                        // scalar cache vs L2
+    if (EB && gK == 1 && !herr && tot != hsx + 1) bad |= 2;                     // K = 1 chain invariant
+    if (pP != P || pPS != PS || pB != B || pK != gK) bad |= 4;                   // args vs Params
+    if (kbase != (unsigned long long)base || (int)ka[2] != P || (int)ka[3] != PS || (int)ka[4] != BA ||
+        (int)ka[5] != pk)
+        bad |= 8;                                                                // preloaded vs memory
+    if (EB && gK == 1 && pe != (hsx + 1 < PS ? hsx + 1 : PS)) bad |= 16;         // host path bound
+    if (kind == 1 && !bad) return;
+    const int r = atomicAdd(&g_dbg_n, 1);
+    if (r >= kDbgRecs) return;
+    unsigned *o = g_dbg[r];
+    const unsigned long long kp = (unsigned long long)ka;
+    const unsigned w[kDbgWords] = {kind, bad, (unsigned)EB | ((unsigned)SEL << 1), (unsigned)t, (unsigned)tot,
+                                   (unsigned)cur, (unsigned)D, (unsigned)herr, (unsigned)tot2, (unsigned)cur2,
+                                   (unsigned)D2, (unsigned)P, (unsigned)PS, (unsigned)BA, (unsigned)pk, (unsigned)K,
+                                   (unsigned)hsx, __float_as_uint(discount), (unsigned)pe, (unsigned)ne,
+                                   (unsigned)pP, (unsigned)pPS, (unsigned)pB, (unsigned)pK,
+                                   (unsigned)kp, (unsigned)(kp >> 32), (unsigned)kbase, (unsigned)(kbase >> 32),
+                                   (unsigned)(unsigned long long)base, (unsigned)((unsigned long long)base >> 32),
+                                   (unsigned)err, (unsigned)(unsigned long long)reward};
+    for (int k = 0; k < kDbgWords; ++k) o[k] = w[k];
+    (void)value;
+    (void)pool;
+}
+#define MZ_SITE(n) atomicOr(&g_dbg_sites, 1u << (n))
+#else
+#define MZ_SITE(n) ((void)0)
+#endif
+
 #ifdef __HIP_DEVICE_COMPILE__
 typedef const __attribute__((address_space(4))) Params cParams;
 typedef const __attribute__((address_space(4))) TreeHdr cTreeHdr;
@@ -989,6 +1040,7 @@ __device__ __forceinline__ void backup(const Geo &g, const Dev &d, Lds &s, int t
     for (int i0 = 0; i0 <= D;) {
         if (cnt == 0) {
             err |= kErrPath;
+            MZ_SITE(1);
             return;
         }
         unsigned long long w0s = 0;
@@ -1059,6 +1111,7 @@ __device__ __forceinline__ void backup(const Geo &g, const Dev &d, Lds &s, int t
             int2 *G = gV + (size_t)n * g.E;
             if (nv + 1 > g.E) {
                 err |= kErrPath;
+                MZ_SITE(2);
                 pos = nv;  // no shift
             } else {
                 G[pos] = make_int2(dep, f2i(key));
@@ -1351,6 +1404,7 @@ __device__ __forceinline__ void walk_precomputed(const Geo &g, const Dev &d, Lds
             }
             if (D + 1 >= g.PS) {
                 err |= kErrPath;
+                MZ_SITE(3);
                 break;
             }
             x = v;
@@ -1491,6 +1545,7 @@ __device__ __forceinline__ void walk_levels(const Geo &g, const Dev &d, Lds &s, 
         }
         if (D + 1 >= g.PS) {
             err |= kErrPath;
+            MZ_SITE(4);
             break;
         }
         x = uni(fc + ci);
@@ -1560,7 +1615,7 @@ __device__ __forceinline__ void select_walk(const Geo &g, const Dev &d, Lds &s, 
     if (g.K == 1) {
         const int D = tot - 1;
         if (D < 1) err |= kErrRoot;
-        if (D + 1 > g.PS) err |= kErrPath;
+        if (D + 1 > g.PS) { err |= kErrPath; MZ_SITE(5); }
         int words = 0;
         if (!err) {
             const int root_visit = uni(s.A[0].x);
@@ -1862,6 +1917,14 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         wait_vm();
     }
     stamp(ts, 1);
+#ifdef MZ_ARGCHECK
+    // diagnostic build (graph-replay investigation): the scalar-cache header against an L2 read of
+    // the same words, the K = 1 chain invariant tot == hsx + 1 on entry, and the preloaded
+    // arguments against the Params block and the kernel-argument memory
+    if (wv == 0 && l == 0)
+        argcheck_record(1, EB, SEL, t, base, P, PS, BA, pk, K, hsx, discount, pe, ne, d.hdr() + t, h.tot, h.cursor,
+                        h.D, h.err, (const unsigned *)__builtin_amdgcn_kernarg_segment_ptr(), reward, value, pool, 0);
+#endif
 #ifdef MZ_ABL_ROUND1  // ablation (timing experiments only): launch + round 1, nothing else
     if (true) {
         wait_vm();
@@ -2170,10 +2233,19 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
     wait_lds();
     if (l < kStatN) st[l] = st_old + xst[l] + (EB ? xst[MZ_S_COUNT + l] : 0ll);
     if (l == 0 && err) atomicOr(d.err(), err);
+#ifdef MZ_ARGCHECK
+    if (l == 0 && err)
+        argcheck_record(2 + wv, EB, SEL, t, base, P, PS, BA, pk, K, hsx, discount, pe, ne, d.hdr() + t, h.tot,
+                        h.cursor, h.D, 0, (const unsigned *)__builtin_amdgcn_kernarg_segment_ptr(), reward, value, pool,
+                        err);
+#endif
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
-__global__ void k_set_seed(unsigned *seed, unsigned v) { *seed = v; }
+// One device word, set by a kernel.  Captured search graphs never hold a runtime memset node: under
+// the HIP runtime's graph packet capture, a replayed hipMemsetAsync node can write a stale fill
+// pattern once enough ordinary launches have run (scripts/memset_graph_repro.hip).
+__global__ void k_set_word(unsigned *w, unsigned v) { *w = v; }
 
 // Small device-to-device copies of readback fields: one launch of this kernel is cheaper inside
 // a graph than the runtime's blit kernel for a memcpy node (~4 us each in rocprof).
@@ -2282,6 +2354,7 @@ struct mz_batch {
     Geo geo;
     Dev dev;
     hipStream_t stream = nullptr;
+    hipEvent_t order_ev = nullptr;  // orders the old stream's work before the new one's (mz_set_stream)
     std::vector<void *> allocs;
     float *in_dev = nullptr;  // host-input staging [B*(2+3A)]
     int *sel_dev = nullptr;   // select output staging [3B]
@@ -2339,7 +2412,11 @@ int check_device_errors(mz_batch *b) {
     int e = 0;
     HIP_TRY(hipMemcpyAsync(&e, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
-    if (e) return fail(MZ_ERR_RUNTIME, err_message(e));
+    if (e) {
+        char bits[32];
+        std::snprintf(bits, sizeof bits, " (device error word 0x%x)", (unsigned)e);
+        return fail(MZ_ERR_RUNTIME, std::string(err_message(e)) + bits);
+    }
     return MZ_OK;
 }
 
@@ -2463,6 +2540,16 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         default: launch_nc<0>(b, eb, sel, a); break;
     }
     HIP_TRY(hipGetLastError());
+#ifdef MZ_ARGCHECK
+    {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(b->stream, &cs);
+        if (cs == hipStreamCaptureStatusActive)
+            fprintf(stderr, "MZCAPTURE step eb%d sel%d b %p base %p hsx %d pe %d ne %d K %d reward %p pool %p out %p\n",
+                    (int)eb, (int)sel, (void *)b, (void *)b->dev.base, a.hsx, a.pe, a.ne, a.K, (const void *)a.reward,
+                    (const void *)a.pool, (void *)a.idx_x);
+    }
+#endif
     if (eb) {
         b->rb_valid = b->rb_dev_valid = false;
         ++b->expansions;
@@ -2729,13 +2816,29 @@ int mz_destroy(mz_batch *b) {
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     else (void)hipDeviceSynchronize();
     for (void *p : b->allocs) (void)hipFree(p);
+    if (b->order_ev) (void)hipEventDestroy(b->order_ev);
     delete b;
     return MZ_OK;
 }
 
 int mz_set_stream(mz_batch *b, void *stream) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
-    b->stream = (hipStream_t)stream;
+    hipStream_t ns = (hipStream_t)stream;
+    if (ns == b->stream) return MZ_OK;
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    // the new stream waits for the work already queued on the old one (the handle's calls stay in
+    // order), except across a graph capture boundary, where the capture itself orders nothing and
+    // an event from outside the capture may not be waited on
+    hipStreamCaptureStatus co = hipStreamCaptureStatusNone, cn = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(b->stream, &co));
+    HIP_TRY(hipStreamIsCapturing(ns, &cn));
+    if (co == hipStreamCaptureStatusNone && cn == hipStreamCaptureStatusNone) {
+        if (!b->order_ev) HIP_TRY(hipEventCreateWithFlags(&b->order_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(b->order_ev, b->stream));
+        HIP_TRY(hipStreamWaitEvent(ns, b->order_ev, 0));
+    }
+    b->stream = ns;
     return MZ_OK;
 }
 
@@ -2777,7 +2880,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     }
     a.eps = noise_eps;
     a.K = K;
-    HIP_TRY(hipMemsetAsync(b->dev.err(), 0, sizeof(int), b->stream));
+    hipLaunchKernelGGL(k_set_word, dim3(1), dim3(1), 0, b->stream, (unsigned *)b->dev.err(), 0u);
     const size_t jl = (b->N > 1) ? (size_t)((12 * b->NA + 15) & ~15) + 8 * (size_t)b->NA + 4 * (size_t)kWave * b->N : 0;
     hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), jl, b->stream, b->prm, a);
     HIP_TRY(hipGetLastError());
@@ -2902,7 +3005,7 @@ int mz_reseed(mz_batch *b, uint32_t seed) {
     if (rc) return rc;
     b->geo.seed = seed;
     b->prepared = false;
-    hipLaunchKernelGGL(k_set_seed, dim3(1), dim3(1), 0, b->stream, b->dev.seed(), (unsigned)seed);
+    hipLaunchKernelGGL(k_set_word, dim3(1), dim3(1), 0, b->stream, b->dev.seed(), (unsigned)seed);
     HIP_TRY(hipGetLastError());
     return MZ_OK;
 }
@@ -3035,15 +3138,47 @@ int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *ou
     if (mem == MZ_MEM_DEVICE) {
         rc = copy_words(b, out, b->rb_dev + rb_field_base(b, field), n);
         if (rc) return rc;
-        if (degrees)
+        if (degrees) {
             rc = copy_words(b, degrees, b->rb_dev + dego, (size_t)b->B);
             if (rc) return rc;
+        }
         return MZ_OK;
     }
     std::memcpy(out, b->rb_host.data() + rb_field_base(b, field), 4 * n);
     if (degrees) std::memcpy(degrees, b->rb_host.data() + dego, 4 * (size_t)b->B);
     return MZ_OK;
 }
+
+#ifdef MZ_ARGCHECK
+// diagnostic build only: [0] = record count, [1] = kErrPath site bits, then the records
+int mz_debug_dump(unsigned *out, int max_words) {
+    int n = 0;
+    unsigned sites = 0;
+    std::vector<unsigned> rec((size_t)kDbgRecs * kDbgWords);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_dbg_n), sizeof(int)));
+    HIP_TRY(hipMemcpyFromSymbol(&sites, HIP_SYMBOL(g_dbg_sites), sizeof(unsigned)));
+    HIP_TRY(hipMemcpyFromSymbol(rec.data(), HIP_SYMBOL(g_dbg), sizeof(unsigned) * rec.size()));
+    if (max_words < 2) return fail(MZ_ERR_ARG, "buffer too small");
+    out[0] = (unsigned)n;
+    out[1] = sites;
+    for (int k = 0; k + 2 < max_words && k < (int)rec.size(); ++k) out[k + 2] = rec[k];
+    return MZ_OK;
+}
+// diagnostic build only: n words of the arena from the error word on, and the arena's layout
+int mz_debug_peek(mz_batch *b, unsigned *out, int n, unsigned long long *layout) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, b->dev.err(), sizeof(unsigned) * n, hipMemcpyDeviceToHost));
+    layout[0] = (unsigned long long)b->dev.base;
+    layout[1] = (unsigned long long)b->dev.err();
+    layout[2] = (unsigned long long)b->dev.seed();
+    layout[3] = (unsigned long long)b->dev.lp();
+    layout[4] = (unsigned long long)b->dev.T();
+    layout[5] = (unsigned long long)b->dev.hdr();
+    layout[6] = (unsigned long long)b->dev.stats();
+    return MZ_OK;
+}
+#endif
 
 int mz_get_stats(mz_batch *b, int64_t *out) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");

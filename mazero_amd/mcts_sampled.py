@@ -34,7 +34,6 @@ from typing import List, NamedTuple, Tuple
 import numpy as np
 import torch
 
-from . import _hipenv
 from ._capi import MZ_DT_F16, MZ_DT_F32, check
 from .cytree import Tree_batch
 
@@ -123,6 +122,7 @@ class _SearchLoop:
         self.leaf = None
         self.graph = None
         self.runs = 0
+        self.storage = None  # _storage_signature(model) when the loop was made
 
     def load(self, hidden, root_arrays, factor):
         self.root.copy_(hidden.reshape(self.B, -1))
@@ -189,6 +189,11 @@ class _SearchLoop:
 _LOOPS: dict = {}
 
 
+def _storage_signature(model) -> tuple:
+    """Device addresses of the model's parameters and buffers (what a recorded graph reads)."""
+    return tuple(t.data_ptr() for t in model.parameters()) + tuple(t.data_ptr() for t in model.buffers())
+
+
 # One device arena per search geometry, kept across searches and across SampledMCTS instances (the
 # self-play worker makes a new SampledMCTS every environment step, selfplay_worker.py:187); a
 # search reseeds it instead of allocating a new tree batch as the reference does (:89).
@@ -202,10 +207,6 @@ class SampledMCTS:
         self.config = config
         self.np_random = np.random if np_random is None else np_random
         self._lib = lib
-        if use_graph and not _hipenv.GRAPHS_SAFE:
-            warnings.warn("HIP was initialised before mazero_amd was imported without "
-                          "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0: search graphs are disabled (see mazero_amd/_hipenv.py)")
-            use_graph = False
         self.use_graph = use_graph
 
     # ---------------------------------------------------------------------------------------
@@ -246,9 +247,11 @@ class SampledMCTS:
 
     def _tree(self, B, seed, device):
         cfg = self.config
+        # (pb_c_base, pb_c_init) select the handle's pUCT tables, which a graph replay does not
+        # rewrite: a handle serves one pair only
         key = (B, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
-               float(cfg.tree_value_stat_delta_lb), float(cfg.mcts_rho), float(cfg.mcts_lambda), str(device),
-               id(self._lib))
+               float(cfg.tree_value_stat_delta_lb), float(cfg.mcts_rho), float(cfg.mcts_lambda),
+               float(cfg.pb_c_base), float(cfg.pb_c_init), str(device), id(self._lib))
         tb = _TREES.get(key)
         if tb is None:
             tb = Tree_batch(B, 1, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
@@ -289,12 +292,18 @@ class SampledMCTS:
                                                            sampled_tau)
         with torch.cuda.device(dev):
             tb = self._tree(B, seed, dev)
-            key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), tuple(hidden.shape), hidden.dtype)
+            # the discount is a kernel argument of the recorded launches
+            key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), float(disc), tuple(hidden.shape),
+                   hidden.dtype)
             for k in [k for k, v in _LOOPS.items() if v.model_ref() is None]:
                 del _LOOPS[k]  # loops (graph, pool) of models that no longer exist
             st = _LOOPS.get(key)
-            if st is None or st.model_ref() is not model:  # ids are reused once an object is freed
+            sig = _storage_signature(model)
+            # ids are reused once an object is freed; a recorded graph reads the parameters at the
+            # addresses it was recorded with (re-homed weights, weights.FlatWeights, need a new one)
+            if st is None or st.model_ref() is not model or st.storage != sig:
                 st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model)
+                st.storage = sig
             st.load(hidden, (rr, rv, rp, rb, rn), factor)
             with torch.no_grad():
                 if not self.use_graph or st.runs == 0:

@@ -20,6 +20,42 @@ from mazero_amd.mcts_sampled import SampledMCTS  # noqa: E402
 from mazero_amd.nets import SearchConfig, make_net, make_root_batch  # noqa: E402
 
 
+FIELDS = ("kind", "bad", "eb|sel<<1", "t", "tot", "cur", "D", "herr", "tot_l2", "cur_l2", "D_l2", "P", "PS", "BA",
+          "pk", "K", "hsx", "disc", "pe", "ne", "prm_P", "prm_PS", "prm_B", "prm_K", "ka_lo", "ka_hi", "kmem_base_lo",
+          "kmem_base_hi", "base_lo", "base_hi", "err", "reward_lo")
+
+
+def dump_records():
+    """MZ_ARGCHECK builds: the device-side records of inconsistent launches (kind 1: on entry,
+    kind 2/3: wave 0/1 set an error) and the kErrPath site bits."""
+    import ctypes as C
+    from mazero_amd._lib import load
+    lib = load()
+    try:
+        fn = lib.mz_debug_dump
+    except AttributeError:
+        return
+    buf = (C.c_uint * (2 + 64 * 32))()
+    fn(buf, len(buf))
+    n, sites = buf[0], buf[1]
+    print(f"argcheck: {n} records, kErrPath sites {sites:#x}", flush=True)
+    from mazero_amd import mcts_sampled
+    peek = getattr(lib, "mz_debug_peek", None)
+    if peek is not None:
+        for tb in list(mcts_sampled._TREES.values()):
+            words = (C.c_uint * 2048)()
+            lay = (C.c_ulonglong * 8)()
+            peek(tb._h, words, 2048, lay)
+            print("arena base %#x err %#x seed %#x lp %#x T %#x hdr %#x stats %#x" % tuple(lay[:7]), flush=True)
+            nz = [(i, words[i]) for i in range(2048) if words[i]]
+            print(f"  nonzero words from err on ({len(nz)}): " +
+                  " ".join(f"+{4 * i}:{v:#x}" for i, v in nz[:96]), flush=True)
+    for r in range(min(n, 64)):
+        w = buf[2 + 32 * r: 2 + 32 * (r + 1)]
+        print("  " + " ".join(f"{k}={v:#x}" if k.endswith(("lo", "hi", "BA", "pk")) else f"{k}={v}"
+                              for k, v in zip(FIELDS, w)), flush=True)
+
+
 def main():
     n_graph = int(sys.argv[1]) if len(sys.argv) > 1 else 7
     n_eager = int(sys.argv[2]) if len(sys.argv) > 2 else 3
@@ -41,6 +77,7 @@ def main():
                                        device=dev, add_noise=True)
                 except RuntimeError as e:
                     print(f"phase graph={use_graph} step {i} agent {agent}: {e}", flush=True)
+                    dump_records()
                     return 3
                 acts[:, agent] = [int(a[np.argmax(v), 0]) for a, v in zip(r.sampled_actions, r.sampled_visit_count)]
     bad = 0
@@ -61,6 +98,7 @@ def main():
             except RuntimeError as e:
                 print(f"test-final agent {agent}: ERR {e}; factor range "
                       f"{None if fac is None else (int(fac.min()), int(fac.max()))}", flush=True)
+                dump_records()
                 return 1
             for i in range(B):
                 pos, _ = select_action(got.sampled_visit_count[i], 1.0, False, rs_d)
@@ -90,6 +128,7 @@ def main():
                 np.array_equal(a, b) for a, b in zip(g[1], e[1]))
             print(f"final {f} agent {agent}: graph vs eager {'same' if same else 'DIFFER'}", flush=True)
             bad += 0 if same else 1
+    dump_records()
     print(f"done: {bad} bad", flush=True)
     return 1 if bad else 0
 

@@ -5,9 +5,9 @@
 
 FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (TCC_EA0_RDREQ / _WRREQ based).  Per
 MI355X_MICROARCH.md §HBM, FETCH_SIZE reads half the bytes of a wide (16 B/lane) coalesced stream
-and other widths are uncalibrated; both the raw per-launch values and the fetch-doubled upper
-estimate are recorded, and `fused_bytes_per_launch` (what bench.py reports as roofline.traffic)
-is the raw FETCH_SIZE + WRITE_SIZE in bytes.
+and other widths are uncalibrated; both are recorded per launch: `fused_bytes_per_launch` is the
+raw FETCH_SIZE + WRITE_SIZE in bytes, `fused_bytes_per_launch_corrected` = 2 x FETCH_SIZE +
+WRITE_SIZE (the guide's correction, what bench.py reports as roofline.traffic).
 """
 from __future__ import annotations
 
@@ -56,7 +56,7 @@ def main():
     out.setdefault("workloads", {})[key] = dict(
         kernels=kernels,
         fused_bytes_per_launch=None if not fused else round((fused["fetch_kb"] + fused["write_kb"]) * 1024),
-        fused_bytes_per_launch_fetch_doubled=None if not fused else round((2 * fused["fetch_kb"] + fused["write_kb"]) * 1024),
+        fused_bytes_per_launch_corrected=None if not fused else round((2 * fused["fetch_kb"] + fused["write_kb"]) * 1024),
         note="FETCH_SIZE/WRITE_SIZE in KB per dispatch, means over all dispatches of the profiled run",
     )
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)

@@ -27,9 +27,44 @@ def test_cpu_baseline_fields(port_lib):
     rng = np.random.default_rng(0)
     B, A, K, S, N = 16, 9, 1, 10, 3
     inputs = [make_search_inputs(rng, B, A, S) for _ in range(N)]
-    r = bench.cpu_baseline(inputs, B, A, K, S, N, 0.2)
+    r = bench.cpu_baseline(inputs, B, A, K, S, N, 0.4, procs=2)
     assert r is not None
     assert r["unit"] == "simulations/s" and r["cores"] == 1 and r["kind"] in ("reference", "port")
     assert r["value"] > 0 and "sims" in r["sample"]
     mc = r["multi_core"]
-    assert mc["value"] > 0 and 1 <= mc["threads"] <= 16
+    assert mc["value"] > 0 and mc["processes"] == 2 and mc["cores"] == 2
+
+
+def test_gpus_flag_spawns_ranks(port_lib):
+    """`bench.py --gpus 2` without torchrun starts two ranks itself (torch.distributed.run), each
+    rank reports the job's world size, and rank 0 prints one JSON line with the weak (headline) and
+    strong-scaling legs.  --backend port keeps it on the CPU (gloo): the plumbing, not a measurement."""
+    import json
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "port", "--roots", "8",
+           "--sims", "6", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["roots_total"] == 16 and line["config"]["roots_per_gpu"] == 8
+    st = line["strong_scaling"]
+    assert st["roots_total"] == 8 and st["roots_per_gpu"] == 4 and st["value"] > 0
+    assert line["value"] > 0
+
+
+def test_world_size_mismatch_fails(port_lib):
+    """Under a launcher whose world size differs from --gpus, bench.py refuses to report."""
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "port", "--roots", "4",
+           "--sims", "4", "--steps", "1", "--no-cpu"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "--gpus 2" in (r.stderr + r.stdout)

@@ -297,6 +297,74 @@ def test_driver_device_outputs_and_reuse(port_lib):
 
 
 @pytest.mark.gpu
+def test_graph_reuse_keys_on_search_constants(port_lib):
+    """Two configurations of one shape that differ only in discount, then only in pb_c_init /
+    pb_c_base, searched alternately (eager, capture, replays): every search matches the oracle
+    with its own constants (the discount is a recorded kernel argument, the pUCT constants pick the
+    device tables, which a replay does not rewrite)."""
+    import dataclasses
+
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, B, S, cur = 3, 9, 32, 12, 0
+    dev = torch.device("cuda", 0)
+    base = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=3)
+    cfgs = [base, dataclasses.replace(base, discount=0.9), dataclasses.replace(base, pb_c_init=2.5, pb_c_base=500.0)]
+    net = make_net(N, A, seed=31, device=dev)
+    for step in range(3):
+        for j, cfg in enumerate(cfgs):
+            out, legal = make_root_batch(net, B, 64, seed=200 + 10 * step + j, device=dev, legal_zero_frac=0.2)
+            rs_o, rs_d = np.random.RandomState(step), np.random.RandomState(step)
+            exp = OracleSampledMCTS(cfg, rs_o, port_lib).batch_search(net, out, cur, None, N, legal, device=dev,
+                                                                       add_noise=True)
+            got = SampledMCTS(cfg, rs_d).batch_search(net, out, cur, None, N, legal, device=dev, add_noise=True)
+            _compare_outputs(got, exp)
+
+
+@pytest.mark.gpu
+def test_graph_after_weights_rehomed(port_lib):
+    """A search graph recorded before weights.FlatWeights re-homes the model's parameters is not
+    replayed against the freed storage: the next search records a new graph and matches the
+    oracle with the re-homed (and then updated) weights."""
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+    from mazero_amd.weights import FlatWeights
+
+    N, A, B, S, cur = 3, 9, 32, 12, 1
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=1)
+    net = make_net(N, A, seed=41, device=dev)
+    factor = np.zeros((B, cur), np.int32)
+
+    def check(step):
+        out, legal = make_root_batch(net, B, 64, seed=300 + step, device=dev, legal_zero_frac=0.2)
+        rs_o, rs_d = np.random.RandomState(step), np.random.RandomState(step)
+        exp = OracleSampledMCTS(cfg, rs_o, port_lib).batch_search(net, out, cur, factor, N, legal, device=dev,
+                                                                   add_noise=True)
+        got = SampledMCTS(cfg, rs_d).batch_search(net, out, cur, factor, N, legal, device=dev, add_noise=True)
+        _compare_outputs(got, exp)
+
+    for step in range(3):  # eager, capture + replay, replay
+        check(step)
+    flat = FlatWeights(net)  # frees the parameters' old storage
+    torch.cuda.empty_cache()
+    for step in range(3, 5):
+        check(step)
+    with torch.no_grad():  # new weights written in place (what a broadcast does)
+        for f in flat.tensors():
+            f.mul_(0.5)
+    for step in range(5, 7):
+        check(step)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K", [1, 5])
 def test_driver_graph_replay_matches_oracle(K, port_lib):
     """Repeated searches of one configuration: the first runs eagerly, the second is captured into
@@ -325,17 +393,18 @@ def test_driver_graph_replay_matches_oracle(K, port_lib):
 @pytest.mark.gpu
 def test_graph_replay_after_eager_launches(port_lib):
     """A captured search graph replayed after thousands of ordinary launches (eager searches of the
-    same configuration) still matches the oracle.  Earlier in round 1 this exact sequence failed
-    in agent 1's replay under the runtime's graph packet capture (mazero_amd/_hipenv.py)."""
+    same configuration, then the oracle's eager network calls) still matches the oracle, under the
+    HIP runtime's default graph packet capture.  In round 1 this sequence failed in agent 1's
+    replay: the graph then held a hipMemsetAsync node (clearing the error word), and under packet
+    capture a replayed memset node wrote a stale fill pattern (0x78787878) once enough ordinary
+    work had run (scripts/memset_graph_repro.hip).  Captured paths now set words with a kernel."""
     import torch
 
     from consume import eps_greedy_given, select_action
     from driver import OracleSampledMCTS
-    from mazero_amd import _hipenv
     from mazero_amd.mcts_sampled import SampledMCTS
     from mazero_amd.nets import SearchConfig, make_net, make_root_batch
 
-    assert _hipenv.GRAPHS_SAFE
     N, A, B, S = 3, 9, 256, 50
     dev = torch.device("cuda", 0)
     cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=1)
@@ -350,24 +419,22 @@ def test_graph_replay_after_eager_launches(port_lib):
                 r = m.batch_search(net, out, agent, acts[:, :agent].copy() if agent else None, N, legal, device=dev,
                                    add_noise=True)
                 acts[:, agent] = [int(a[np.argmax(v), 0]) for a, v in zip(r.sampled_actions, r.sampled_visit_count)]
-    # a self-play step replaying the graphs, against the oracle driver
+    # a self-play step: per agent the oracle driver first (eager network calls on the device), then
+    # the graph replay of the device driver on the same inputs
     ur = np.random.default_rng(1)
     u_eps, u_cat = ur.random((N, B)).astype(np.float32), ur.random((N, B))
     rs_o, rs_d = np.random.default_rng(3), np.random.default_rng(3)
     oracle, drv = OracleSampledMCTS(cfg, rs_o, port_lib), SampledMCTS(cfg, rs_d)
     out, legal = roots[0]
     acts = np.full((B, N), -1, np.int32)
-    got, factors = [], []
-    for agent in range(N):  # the device step first: the oracle's eager network calls would move the launch ring
-        factors.append(acts[:, :agent].copy() if agent else None)
-        got.append(drv.batch_search(net, out, agent, factors[-1], N, legal, device=dev, add_noise=True))
-        for i in range(B):
-            pos, _ = select_action(got[-1].sampled_visit_count[i], 1.0, False, rs_d)
-            acts[i, agent] = eps_greedy_given(got[-1].sampled_actions[i][pos, 0], legal[i, agent], 0.1,
-                                              u_eps[agent, i], u_cat[agent, i])
     for agent in range(N):
-        exp = oracle.batch_search(net, out, agent, factors[agent], N, legal, device=dev, add_noise=True)
-        _compare_outputs(got[agent], exp)
+        fac = acts[:, :agent].copy() if agent else None
+        exp = oracle.batch_search(net, out, agent, fac, N, legal, device=dev, add_noise=True)
+        got = drv.batch_search(net, out, agent, fac, N, legal, device=dev, add_noise=True)
+        _compare_outputs(got, exp)
         for i in range(B):
             select_action(exp["sampled_visit_count"][i], 1.0, False, rs_o)
+            pos, _ = select_action(got.sampled_visit_count[i], 1.0, False, rs_d)
+            acts[i, agent] = eps_greedy_given(got.sampled_actions[i][pos, 0], legal[i, agent], 0.1,
+                                              u_eps[agent, i], u_cat[agent, i])
     assert rs_o.random() == rs_d.random()
