@@ -44,6 +44,15 @@ def _dev_i32(x, dev) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32)).to(dev)
 
 
+def _root_uniforms(mcts, B: int) -> np.ndarray:
+    """select_action's np_random.choice doubles for B roots (a sharded driver draws the whole
+    batch's and keeps its own, mcts_sampled.SampledMCTS.draw_root_uniforms)."""
+    fn = getattr(mcts, "draw_root_uniforms", None)
+    if fn is not None:
+        return fn(B)
+    return np.asarray(mcts.np_random.random(B), dtype=np.float64)
+
+
 def _tree(out: DeviceSearchOutput):
     if out.tree is None:
         raise ValueError("DeviceSearchOutput without its tree handle (use SampledMCTS.batch_search_device)")
@@ -148,7 +157,7 @@ def selfplay_decisions(mcts, model, network_output, true_num_agents: int, legal_
                                        add_noise=True, sampled_tau=sampled_tau)
         outs.append(out)
         # select_action's np_random.choice: one double per root, in root order (:240-247)
-        u = torch.from_numpy(np.asarray(mcts.np_random.random(B), dtype=np.float64)).to(dev)
+        u = torch.from_numpy(_root_uniforms(mcts, B)).to(dev)
         with torch.cuda.device(dev):
             _, act, ent = select_actions(out, u, temperature, deterministic=False)
             eps_greedy(out, act, legal[:, k, :], greedy_epsilon, u_eps[k], u_cat[k])  # :250-254

@@ -203,10 +203,22 @@ _TREES: dict = {}
 class SampledMCTS:
     """mcts_sampled.py:29-32.  `lib` selects the tree library (default: the MI355X product)."""
 
-    def __init__(self, config, np_random: np.random.RandomState = None, *, lib=None, use_graph: bool = True):
+    def __init__(self, config, np_random: np.random.RandomState = None, *, lib=None, use_graph: bool = True,
+                 root_shard: Tuple[int, int, int] = None):
+        """`root_shard` = (lo, hi, total): this instance searches roots [lo, hi) of a batch of `total`
+        roots sharded over ranks (mazero_amd.workers).  Every rank holds the same `np_random` state;
+        the per-root draws (Dirichlet noise here, select_action's uniforms in consume) are drawn for
+        the whole batch and sliced, and tree i is seeded with its global index, so a rank's results
+        equal rows [lo, hi) of the unsharded search."""
         self.config = config
         self.np_random = np.random if np_random is None else np_random
         self._lib = lib
+        if root_shard is not None:
+            lo, hi, total = (int(x) for x in root_shard)
+            if not 0 <= lo < hi <= total:
+                raise ValueError(f"bad root shard {root_shard}")
+            root_shard = (lo, hi, total)
+        self.root_shard = root_shard
         self.use_graph = use_graph
 
     # ---------------------------------------------------------------------------------------
@@ -222,7 +234,8 @@ class SampledMCTS:
         probs = np.exp(logits - np.max(logits, axis=-1, keepdims=True))
         probs = probs / np.sum(probs, axis=-1, keepdims=True)
         # Dirichlet noise is always drawn, then disabled for evaluation, :68-70
-        noises = self.np_random.dirichlet([alpha] * A, B).astype(np.float32).reshape(B, 1, A)
+        noises = self.draw_rows(lambda n: self.np_random.dirichlet([alpha] * A, n), B)
+        noises = noises.astype(np.float32).reshape(B, 1, A)
         if not add_noise:
             eps = 0.0
         mask = None
@@ -245,21 +258,39 @@ class SampledMCTS:
         return (rewards, values, probs.astype(np.float32), beta.astype(np.float32), eps,
                 noises.astype(np.float32, copy=False)), seed
 
+    def draw_rows(self, draw, B: int) -> np.ndarray:
+        """`draw(n)` -> n per-root rows from np_random; with a root shard the whole batch's rows are
+        drawn (same generator consumption on every rank) and this shard's rows returned."""
+        if self.root_shard is None:
+            return draw(B)
+        lo, hi, total = self.root_shard
+        if hi - lo != B:
+            raise ValueError(f"batch of {B} roots but the root shard is [{lo}, {hi})")
+        return draw(total)[lo:hi]
+
+    def draw_root_uniforms(self, B: int) -> np.ndarray:
+        """One double per root in root order, as B np_random.choice(n, p) calls draw them."""
+        return np.asarray(self.draw_rows(lambda n: self.np_random.random(n), B), dtype=np.float64)
+
     def _tree(self, B, seed, device):
         cfg = self.config
         # (pb_c_base, pb_c_init) select the handle's pUCT tables, which a graph replay does not
         # rewrite: a handle serves one pair only
         key = (B, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
                float(cfg.tree_value_stat_delta_lb), float(cfg.mcts_rho), float(cfg.mcts_lambda),
-               float(cfg.pb_c_base), float(cfg.pb_c_init), str(device), id(self._lib))
+               float(cfg.pb_c_base), float(cfg.pb_c_init), str(device), id(self._lib), self._root_offset())
         tb = _TREES.get(key)
         if tb is None:
             tb = Tree_batch(B, 1, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
-                            cfg.tree_value_stat_delta_lb, int(seed), cfg.mcts_rho, cfg.mcts_lambda, lib=self._lib)
+                            cfg.tree_value_stat_delta_lb, int(seed), cfg.mcts_rho, cfg.mcts_lambda,
+                            root_offset=self._root_offset(), lib=self._lib)
             _TREES[key] = tb
         else:
             tb.reseed(int(seed))
         return tb
+
+    def _root_offset(self) -> int:
+        return 0 if self.root_shard is None else self.root_shard[0]
 
     # ---------------------------------------------------------------------------------------
     def batch_search(self, model, network_output, current_agent_idx: int, factor: np.ndarray,

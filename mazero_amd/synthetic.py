@@ -141,9 +141,11 @@ def make_search_inputs(
     )
 
 
-def run_search(tb, inp: SearchInputs, K: int, knobs: dict | None = None, record: bool = True):
+def run_search(tb, inp: SearchInputs, K: int, knobs: dict | None = None, record: bool = True,
+               per_sim: bool = True):
     """Drive a Tree_batch-compatible object through one full search (mcts_sampled.py:89-191
-    minus the network), returning every selection and the final readbacks.
+    minus the network), returning every selection and the final readbacks (`record`), plus the
+    root values and marginal visit counts after every simulation (`per_sim`).
 
     `tb` needs the cytree.Tree_batch methods (prepare, batch_selection,
     batch_expansion_and_backup, get_roots_*).
@@ -156,8 +158,8 @@ def run_search(tb, inp: SearchInputs, K: int, knobs: dict | None = None, record:
     S, B = inp.S, inp.B
     sel_idx = np.zeros((S, B), np.int32)
     sel_act = np.zeros((S, B), np.int32)
-    root_values = np.zeros((S, B), np.float32)
-    marginal = np.zeros((S, B, inp.A), np.int32)
+    root_values = np.zeros((S, B), np.float32) if per_sim else None
+    marginal = np.zeros((S, B, inp.A), np.int32) if per_sim else None
     for s in range(S):
         ix, iy, act = tb.batch_selection(c2, c1, g)
         if record:
@@ -165,10 +167,12 @@ def run_search(tb, inp: SearchInputs, K: int, knobs: dict | None = None, record:
             sel_act[s] = np.asarray(act, np.int32).reshape(B, -1)[:, 0]
             assert list(iy) == list(range(B))
         tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
-        if record:
+        if record and per_sim:
             root_values[s] = tb.get_roots_values()
             marginal[s] = tb.get_roots_marginal_visit_count().reshape(B, -1)[:, : inp.A]
-    out = dict(sel_idx=sel_idx, sel_act=sel_act, root_values_per_sim=root_values, marginal_per_sim=marginal)
+    out = dict(sel_idx=sel_idx, sel_act=sel_act)
+    if per_sim:
+        out.update(root_values_per_sim=root_values, marginal_per_sim=marginal)
     if record:
         out.update(readbacks(tb, g))
     return out
@@ -209,3 +213,21 @@ def readbacks(tb, discount: float) -> dict:
                 arr[i, : len(a)] = a
         res["sampled_" + name] = arr
     return res
+
+
+def inputs_digest(inp: SearchInputs) -> str:
+    """SHA-256 over every input array of a search (shape, dtype and bytes, in a fixed order) and the
+    tree seed: fixtures that regenerate their inputs from a seed check it first, so a change in
+    numpy's generators cannot pass unnoticed."""
+    import hashlib
+
+    h = hashlib.sha256()
+    h.update(np.int64([inp.B, inp.A, inp.S, inp.seed]).tobytes())
+    h.update(np.float64([inp.noise_eps]).tobytes())
+    for a in (inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, inp.root_noise, inp.reward, inp.value,
+              inp.policy, inp.beta):
+        a = np.ascontiguousarray(a)
+        h.update(str((a.shape, a.dtype.str)).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+

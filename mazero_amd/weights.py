@@ -32,18 +32,21 @@ class FlatWeights:
 
     def __init__(self, model: torch.nn.Module):
         self.model = model
-        entries = [(m, n, p, True) for m in model.modules() for n, p in m._parameters.items() if p is not None]
-        entries += [(m, n, b, False) for m in model.modules() for n, b in m._buffers.items()
+        mods = list(model.named_modules())
+        entries = [(m, n, p, True, f"{mn}.{n}" if mn else n) for mn, m in mods for n, p in m._parameters.items()
+                   if p is not None]
+        entries += [(m, n, b, False, f"{mn}.{n}" if mn else n) for mn, m in mods for n, b in m._buffers.items()
                     if b is not None and b.is_floating_point()]
         by_dtype: Dict[torch.dtype, List] = {}
         for e in entries:
             by_dtype.setdefault(e[2].dtype, []).append(e)
         self.flats: Dict[torch.dtype, torch.Tensor] = {}
+        self.index: Dict[str, tuple] = {}  # state_dict key -> (dtype, offset, numel)
         for dtype, es in by_dtype.items():
             total = sum(e[2].numel() for e in es)
             flat = torch.empty(total, dtype=dtype, device=es[0][2].device)
             off = 0
-            for mod, name, t, is_param in es:
+            for mod, name, t, is_param, full in es:
                 n = t.numel()
                 view = flat[off:off + n].view_as(t)
                 view.copy_(t.detach())
@@ -51,8 +54,18 @@ class FlatWeights:
                     mod._parameters[name].data = view
                 else:
                     mod._buffers[name] = view
+                self.index[full] = (dtype, off, n)
                 off += n
             self.flats[dtype] = flat
+
+    def load_into(self, flats: Dict[torch.dtype, torch.Tensor], state_dict) -> None:
+        """Copy a state_dict (the learner's weights) into flat buffers laid out like these."""
+        missing = set(self.index) - set(state_dict)
+        if missing:
+            raise KeyError(f"state_dict lacks {sorted(missing)[:3]}")
+        with torch.no_grad():
+            for k, (dtype, off, n) in self.index.items():
+                flats[dtype][off:off + n].copy_(torch.as_tensor(state_dict[k]).reshape(-1))
 
     @property
     def numel(self) -> int:
@@ -65,29 +78,60 @@ class FlatWeights:
 class WeightBroadcaster:
     """Periodic weight broadcast from rank `src`.
 
-    `publish(model_index)` on `src` marks the current weights as checkpoint `model_index`.
-    `sync()` is called by every rank before an environment step: the newest index goes out first,
-    then the weights, but only when the index changed since the last sync.  It returns the model
-    index each rank now holds."""
+    `publish(model_index)` on `src` marks the current weights as checkpoint `model_index` (the
+    learner's trained-steps counter, shared_storage.get_counter).  `sync()` is called by every rank
+    before an environment step: the newest index goes out first, then the weights, but only when
+    the index crossed into a new checkpoint interval since this rank's last weights -- the rule of
+    `_update_model_before_step` (selfplay_worker.py:371-375):
+    `last_model_index // checkpoint_interval < trained_steps // checkpoint_interval`.
+    With checkpoint_interval = 1 every new index brings new weights.  It returns the model index
+    of the weights each rank now holds."""
 
-    def __init__(self, model: torch.nn.Module, src: int = 0, group=None):
+    def __init__(self, model: torch.nn.Module, src: int = 0, group=None, checkpoint_interval: int = 1):
+        if checkpoint_interval < 1:
+            raise ValueError("checkpoint_interval must be >= 1")
         self.flat = FlatWeights(model)
         self.src = src
         self.group = group
+        self.checkpoint_interval = int(checkpoint_interval)
         dev = next(iter(self.flat.flats.values())).device
         self._idx = torch.full((1,), -1, dtype=torch.int64, device=dev)
         self.model_index = -1
+        self.syncs = 0  # weight transfers so far
+        self._stage = None  # staged learner weights (source rank)
+        self._staged = False
 
-    def publish(self, model_index: int) -> None:
+    def publish(self, model_index: int, state_dict=None) -> None:
+        """Mark checkpoint `model_index` (SharedStorage.set_weights, core/storage.py:68-80).  With
+        `state_dict` (the learner's weights) they are staged and become the live weights -- on this
+        rank too -- at the next sync that transfers; without it the live model's current weights
+        are the checkpoint."""
         if dist.get_rank(self.group) != self.src:
             raise RuntimeError("only the source rank publishes weights")
+        if state_dict is not None:
+            if self._stage is None:
+                self._stage = {k: torch.empty_like(v) for k, v in self.flat.flats.items()}
+            self.flat.load_into(self._stage, state_dict)
+            self._staged = True
         self._idx.fill_(int(model_index))
+
+    def _due(self, new: int) -> bool:
+        ci = self.checkpoint_interval
+        if self.model_index < 0:
+            return new >= 0
+        return self.model_index // ci < new // ci
 
     def sync(self) -> int:
         dist.broadcast(self._idx, src=self.src, group=self.group)
         new = int(self._idx.item())
-        if new != self.model_index:
+        if new != self.model_index and self._due(new):  # the same decision on every rank
+            if self._staged:
+                with torch.no_grad():
+                    for k, f in self.flat.flats.items():
+                        f.copy_(self._stage[k])
+                self._staged = False
             for t in self.flat.tensors():
                 dist.broadcast(t, src=self.src, group=self.group)
             self.model_index = new
+            self.syncs += 1
         return self.model_index

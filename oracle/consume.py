@@ -59,7 +59,7 @@ def eps_greedy_given(greedy_action, legal_action_mask, eps, u_eps, u_cat):
 
 
 def selfplay_step(mcts, model, network_output, true_num_agents, legal_actions_lst, temperature, sampled_tau,
-                  greedy_epsilon, np_random, u_eps, u_cat, device=None):
+                  greedy_epsilon, np_random, u_eps, u_cat, device=None, root_shard=None):
     """core/selfplay_worker.py:189-293 for the active envs of one step.  `mcts` is an oracle
     driver (oracle/driver.py) sharing `np_random`; u_eps / u_cat [N, B] replace the per-root
     torch draws."""
@@ -74,6 +74,8 @@ def selfplay_step(mcts, model, network_output, true_num_agents, legal_actions_ls
         so = mcts.batch_search(model, network_output, agent_idx, factor, N, legal_actions_lst, device=device,
                                add_noise=True, sampled_tau=sampled_tau)
         outs.append(so)
+        if root_shard is not None:  # the other ranks' roots draw before and after this shard's
+            np_random.random(root_shard[0])
         for i in range(B):
             sampled_actions = so["sampled_actions"][i]
             sampled_visit_counts = so["sampled_visit_count"][i]
@@ -90,6 +92,8 @@ def selfplay_step(mcts, model, network_output, true_num_agents, legal_actions_ls
                                             u_eps[agent_idx][i], u_cat[agent_idx][i])
             temp_agent_actions[i, agent_idx] = agent_action
             temp_entropies[i][agent_idx] = visit_entropy_per_agent
+        if root_shard is not None:
+            np_random.random(root_shard[2] - root_shard[1])
     prob = np.zeros(B)
     visit_entropy = np.zeros((B, N))
     for i in range(B):

@@ -28,12 +28,26 @@ def _np(x):
 
 
 class OracleSampledMCTS:
-    def __init__(self, config, np_random, tree_lib, record: bool = False):
+    def __init__(self, config, np_random, tree_lib, record: bool = False, root_shard=None):
         self.config = config
         self.np_random = np_random
         self.lib = tree_lib
         self.record = record
         self.trace = []  # per simulation: the tree inputs (for replay / diagnosis)
+        # (lo, hi, total): rows [lo, hi) of a batch sharded over ranks -- per-root draws are made
+        # for the whole batch and sliced, trees seeded with their global index (needs the CPU port:
+        # the reference ctree has no root offset)
+        self.root_shard = root_shard
+
+    def _rows(self, draw, B):
+        if self.root_shard is None:
+            return draw(B)
+        lo, hi, total = self.root_shard
+        assert hi - lo == B
+        return draw(total)[lo:hi]
+
+    def draw_root_uniforms(self, B):
+        return np.asarray(self._rows(lambda n: self.np_random.random(n), B), dtype=np.float64)
 
     def batch_search(self, model, network_output, current_agent_idx, factor, true_num_agents,
                      legal_actions_lst=None, device=None, add_noise=False, sampled_tau=1.0):
@@ -53,7 +67,7 @@ class OracleSampledMCTS:
         logits = _np(network_output.policy_logits)[:, current_agent_idx, :].reshape(B, 1, A)
         probs = np.exp(logits - np.max(logits, axis=-1, keepdims=True))
         probs = probs / np.sum(probs, axis=-1, keepdims=True)
-        noises = self.np_random.dirichlet([alpha] * A, B).astype(np.float32).reshape(B, 1, A)
+        noises = self._rows(lambda n: self.np_random.dirichlet([alpha] * A, n), B).astype(np.float32).reshape(B, 1, A)
         if not add_noise:
             eps = 0.0
         if legal_actions_lst is not None:
@@ -68,7 +82,8 @@ class OracleSampledMCTS:
         # mcts_sampled.py:86-106
         pool = [hs0]
         trees = Tree_batch(B, 1, A, K, cfg.num_simulations, cfg.tree_value_stat_delta_lb,
-                           self.np_random.choice(256), rho, lam, lib=self.lib)
+                           self.np_random.choice(256), rho, lam, lib=self.lib,
+                           root_offset=0 if self.root_shard is None else self.root_shard[0])
         beta = probs * (1 - eps) + noises * eps
         beta = beta ** (1 / sampled_tau)
         if legal_actions_lst is not None:

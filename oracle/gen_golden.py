@@ -10,8 +10,13 @@ Runs in the build container (it needs oracle/_ref/libmzref.so, the reference ctr
                                     simulation, all final readbacks)
   tests/golden/kat_libstdcxx.json   libstdc++ mt19937 / discrete_distribution known answers
                                     (oracle/kat_libstdcxx.cpp) + glibc logf pUCT table entries
+  tests/golden/full_<name>.npz      (--full) searches at the BASELINE sizes: the generator seed and
+                                    the SHA-256 of the inputs it yields (synthetic.inputs_digest;
+                                    the inputs themselves are regenerated, not stored), the
+                                    reference's selection idx/action of every simulation and all
+                                    final readbacks
 
-Usage:  make -C oracle && python oracle/gen_golden.py
+Usage:  make -C oracle && python oracle/gen_golden.py [--full]
 """
 from __future__ import annotations
 
@@ -29,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 from mazero_amd import _capi  # noqa: E402
 from mazero_amd.cytree import Tree_batch  # noqa: E402
-from mazero_amd.synthetic import DEFAULTS, make_search_inputs, run_search  # noqa: E402
+from mazero_amd.synthetic import DEFAULTS, inputs_digest, make_search_inputs, run_search  # noqa: E402
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
@@ -52,6 +57,45 @@ CONFIGS = {
     "knobs_rho03": (8, 9, 5, 50, 0.25, 0.0, False, dict(rho=0.3, lam=0.9, delta_lb=0.05)),
     "knobs_rho0": (8, 9, 3, 40, 0.25, 0.0, False, dict(rho=0.0, lam=1.0, discount=0.99)),
 }
+
+
+# BASELINE.json sizes: name: (B, A, K, S, noise_eps, legal_zero_frac, ties)
+FULL = {
+    "3m_k1": (256, 9, 1, 50, 0.25, 0.0, False),
+    "3m_k5": (256, 9, 5, 50, 0.25, 0.0, False),
+    "3m_k10": (256, 9, 10, 50, 0.25, 0.0, False),
+    "3m_k5_ties": (256, 9, 5, 50, 0.25, 0.0, True),
+    "2s3z_k1": (1024, 11, 1, 50, 0.25, 0.0, False),
+    "2s3z_k5": (1024, 11, 5, 50, 0.25, 0.0, False),
+    "3s5z_k5": (512, 15, 5, 100, 0.25, 0.0, False),
+    "3s5z_k10": (512, 15, 10, 100, 0.25, 0.0, False),
+    "3s5z_k5_legal30": (512, 15, 5, 100, 0.25, 0.3, False),
+    "27m_k1": (256, 36, 1, 200, 0.25, 0.0, False),
+    "27m_k5": (256, 36, 5, 200, 0.25, 0.0, False),
+}
+
+
+def full_inputs(name, seed):
+    B, A, K, S, eps, lz, ties = FULL[name]
+    return make_search_inputs(np.random.default_rng(seed), B, A, S, noise_eps=eps, legal_zero_frac=lz, ties=ties), K
+
+
+def record_full(lib, name, seed):
+    inp, K = full_inputs(name, seed)
+    tb = Tree_batch(inp.B, 1, inp.A, K, inp.S, DEFAULTS["delta_lb"], inp.seed, DEFAULTS["rho"], DEFAULTS["lam"],
+                    lib=lib)
+    out = run_search(tb, inp, K, per_sim=False)
+    arrays = dict(
+        cfg=np.array([inp.B, inp.A, K, inp.S, inp.seed], np.int64),
+        gen_seed=np.array([seed], np.int64),
+        gen_args=np.array(FULL[name][4:7], np.float64),  # noise_eps, legal_zero_frac, ties
+        inputs_sha256=np.frombuffer(bytes.fromhex(inputs_digest(inp)), np.uint8),
+    )
+    for k, v in out.items():
+        arrays["out_" + k] = v
+    path = os.path.join(GOLDEN, f"full_{name}.npz")
+    np.savez_compressed(path, **arrays)
+    return path
 
 
 def record(lib, name, cfg, seed):
@@ -108,6 +152,11 @@ def main():
     os.makedirs(GOLDEN, exist_ok=True)
     lib = _capi.bind(C.CDLL(os.path.join(HERE, "_ref", "libmzref.so")))
     assert lib.mz_backend() == b"reference-ctree"
+    if "--full" in sys.argv:
+        for i, name in enumerate(FULL):
+            p = record_full(lib, name, seed=5000 + i)
+            print("wrote", os.path.relpath(p, ROOT), os.path.getsize(p), "bytes", flush=True)
+        return
     for i, (name, cfg) in enumerate(CONFIGS.items()):
         p = record(lib, name, cfg, seed=1000 + i)
         print("wrote", os.path.relpath(p, ROOT), os.path.getsize(p), "bytes")

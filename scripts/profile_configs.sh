@@ -1,0 +1,47 @@
+#!/bin/bash
+# Measurement pass over the BASELINE.json configurations that fit one GPU: for each one
+#   bench.json         bench.py as the driver runs it (headline also with the CPU baseline)
+#   traced.json        bench.py under rocprofv3 --kernel-trace --stats (its own HIP-event timing
+#                      of the fused kernel, taken under the profiler)
+#   trace/             the rocprofv3 kernel trace + stats of that run
+#   pmc_fetch/, pmc_write/   separate --pmc FETCH_SIZE / WRITE_SIZE passes
+# then scripts/pmc_summary.py (-> gpurun_out/pmc_latest.json) and scripts/reconcile.py
+# (-> gpurun_out/prof/summary.json).  CONFIGS="3m_k1 ..." selects a subset.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+R=$(pwd)
+export TMPDIR=/tmp
+mkdir -p gpurun_out/prof
+declare -A ARGS=(
+  [3m_k1]="--map 3m --roots 256 --sims 50 --sampled-times 1"
+  [3m_k5]="--map 3m --roots 256 --sims 50 --sampled-times 5"
+  [2s3z_k1]="--map 2s3z --roots 1024 --sims 50 --sampled-times 1"
+  [3s5z_k5]="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5"
+  [27m_k1]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1"
+  [27m_k5]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5"
+)
+CONFIGS=${CONFIGS:-"3m_k1 3m_k5 2s3z_k1 3s5z_k5 27m_k1 27m_k5"}
+step() {  # log timeout cmd...
+    local log=$1 to=$2; shift 2
+    timeout -k 10 "$to" "$@" > "$log" 2> "$log.err"
+    local rc=$?
+    echo "  $(basename "$log") rc=$rc"
+    [ $rc -ne 0 ] && { tail -5 "$log.err"; exit $rc; }
+    return 0
+}
+for c in $CONFIGS; do
+    a=${ARGS[$c]}
+    d=gpurun_out/prof/$c
+    mkdir -p "$d"
+    echo "== $c ($a)"
+    cpu="--no-cpu"; [ "$c" = 3m_k1 ] && cpu=""
+    step "$d/bench.json" 300 python bench.py $a $cpu
+    step "$d/traced.json" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$d/trace" -o run -- \
+        python3 "$R/bench.py" --no-cpu $a
+    step "$d/pmc_fetch.json" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$d/pmc_fetch" -o run -- \
+        python3 "$R/bench.py" --no-cpu --steps 3 --warmup 1 $a
+    step "$d/pmc_write.json" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/$d/pmc_write" -o run -- \
+        python3 "$R/bench.py" --no-cpu --steps 3 --warmup 1 $a
+    step "$d/pmc_summary.txt" 120 python scripts/pmc_summary.py "$d/pmc_fetch" "$d/pmc_write" --bench-args "$a" \
+        --out gpurun_out/pmc_latest.json
+done
+python scripts/reconcile.py gpurun_out/prof --out gpurun_out/prof/summary.json

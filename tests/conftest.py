@@ -85,3 +85,26 @@ def assert_same(out, expected, where=""):
         if not same:
             bad = np.argwhere(got != v)
             raise AssertionError(f"{where}{k}: {len(bad)} mismatches, first at {bad[:3].tolist()}")
+
+
+def full_fixtures():
+    return sorted(glob.glob(os.path.join(GOLDEN, "full_*.npz")))
+
+
+def load_full(path):
+    """A BASELINE-size fixture (oracle/gen_golden.py --full): the inputs regenerated from the
+    recorded generator seed and checked against the recorded SHA-256, then
+    (SearchInputs, K, expected outputs dict)."""
+    from mazero_amd.synthetic import inputs_digest, make_search_inputs
+
+    z = np.load(path)
+    B, A, K, S, tree_seed = [int(x) for x in z["cfg"]]
+    eps, lz, ties = [float(x) for x in z["gen_args"]]
+    inp = make_search_inputs(np.random.default_rng(int(z["gen_seed"][0])), B, A, S, noise_eps=eps,
+                             legal_zero_frac=lz, ties=bool(ties))
+    assert inp.seed == tree_seed, f"{os.path.basename(path)}: regenerated tree seed differs"
+    assert inputs_digest(inp) == bytes(z["inputs_sha256"]).hex(), (
+        f"{os.path.basename(path)}: regenerated inputs differ from the recorded ones (numpy generator drift)")
+    expected = {k[4:]: z[k] for k in z.files if k.startswith("out_")}
+    return inp, K, expected
+

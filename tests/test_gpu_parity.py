@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import assert_same, golden_traces, load_trace
+from conftest import assert_same, full_fixtures, golden_traces, load_full, load_trace
 
 pytestmark = pytest.mark.gpu
 
@@ -118,6 +118,21 @@ def test_golden_fused_loop(gpu_lib, path):
     assert_same(out, expected, "gpu(fused) ")
 
 
+FULL = full_fixtures()
+
+
+@pytest.mark.parametrize("path", FULL, ids=[os.path.basename(p)[5:-4] for p in FULL])
+def test_baseline_sizes_vs_reference(gpu_lib, path):
+    """The fused device loop against the reference ctree's own outputs at every BASELINE size
+    (oracle/gen_golden.py --full: 3m 256 x 50 K in {1, 5, 10}, 2s3z 1024 x 50 K in {1, 5}, 3s5z
+    512 x 100 K in {5, 10}, 27m 256 x 200 K in {1, 5}, a tie variant and a 30 %-masked variant):
+    selections of every simulation and all final readbacks, bit for bit.  The inputs are
+    regenerated on the box and checked against the recorded SHA-256 first."""
+    inp, K, expected = load_full(path)
+    out, _ = run_fused(make_tb(gpu_lib, inp, K, {}), to_device(inp), K, {})
+    assert_same(out, expected, f"gpu {os.path.basename(path)} ")
+
+
 BIG = [
     ("3m_k1", 256, 9, 1, 50, 0.0),
     ("3m_k5", 256, 9, 5, 50, 0.3),
@@ -134,7 +149,7 @@ BIG = [
 def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     from mazero_amd.synthetic import make_search_inputs, run_search
 
-    rng = np.random.default_rng(hash(name) % 2**32)
+    rng = np.random.default_rng(sum(map(ord, name)) * 7919 + B)
     inp = make_search_inputs(rng, B, A, S, legal_zero_frac=lz)
     knobs = {}
     exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)

@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, assert_same, golden_traces, load_trace
+from conftest import GOLDEN, assert_same, full_fixtures, golden_traces, load_full, load_trace
 
 import ptree
 from mazero_amd.cytree import Tree_batch
@@ -138,3 +138,58 @@ def test_port_joint_action_trees_match_reference(ref_lib, port_lib):
             assert np.array_equal(orf[k].view(np.int32), op[k].view(np.int32)), (name, k)
         for k in ("q", "acts", "vc", "pr", "bh"):
             assert all(np.array_equal(g.view(np.int32), c.view(np.int32)) for g, c in zip(orf[k], op[k])), (name, k)
+
+
+FULL = full_fixtures()
+
+
+@pytest.mark.parametrize("path", FULL, ids=[os.path.basename(p)[5:-4] for p in FULL])
+def test_port_matches_reference_at_baseline_sizes(port_lib, path):
+    """The CPU port against the reference ctree's own outputs at the BASELINE sizes (3m 256 x 50,
+    2s3z 1024 x 50, 3s5z 512 x 100, 27m 256 x 200; ties; 30 % masked actions), recorded by
+    oracle/gen_golden.py --full; the regenerated inputs are checked against the recorded digest."""
+    inp, K, expected = load_full(path)
+    tb = Tree_batch(inp.B, 1, inp.A, K, inp.S, 0.01, inp.seed, 0.75, 0.8, lib=port_lib)
+    assert_same(run_search(tb, inp, K, per_sim=False), expected, "port ")
+
+
+
+def test_port_under_sanitizers():
+    """the CPU restatement built with AddressSanitizer + UBSan (make -C oracle asan)
+    replays every golden trace and three BASELINE-size fixtures bit-exactly with no report (the
+    sanitizer runtime aborts the child process on the first error)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(GOLDEN.rstrip("/"))
+    root = os.path.dirname(root)
+    subprocess.run(["make", "-C", os.path.join(root, "oracle"), "asan"], check=True, stdout=subprocess.DEVNULL)
+    asan = subprocess.check_output(["g++", "-print-file-name=libasan.so"], text=True).strip()
+    if not os.path.isabs(asan):
+        pytest.skip("libasan not available")
+    env = dict(os.environ)
+    env["LD_PRELOAD"] = ":".join(x for x in (asan, os.environ.get("LD_PRELOAD", "")) if x)
+    env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
+    code = f"""
+import ctypes as C, os, sys
+sys.path[:0] = [{root!r}, {os.path.join(root, "tests")!r}, {os.path.join(root, "oracle")!r}]
+from conftest import assert_same, full_fixtures, golden_traces, load_full, load_trace
+from mazero_amd import _capi
+from mazero_amd.cytree import Tree_batch
+from mazero_amd.synthetic import run_search
+lib = _capi.bind(C.CDLL(os.path.join({root!r}, "oracle", "_build", "libmzport_asan.so")))
+n = 0
+for p in golden_traces():
+    inp, knobs, K, exp = load_trace(p)
+    tb = Tree_batch(inp.B, 1, inp.A, K, inp.S, knobs["delta_lb"], inp.seed, knobs["rho"], knobs["lam"], lib=lib)
+    assert_same(run_search(tb, inp, K, knobs), exp, os.path.basename(p)); n += 1
+for p in [f for f in full_fixtures() if any(k in f for k in ("3m_k5_ties", "3m_k10", "27m_k1"))]:
+    inp, K, exp = load_full(p)
+    tb = Tree_batch(inp.B, 1, inp.A, K, inp.S, 0.01, inp.seed, 0.75, 0.8, lib=lib)
+    assert_same(run_search(tb, inp, K, per_sim=False), exp, os.path.basename(p)); n += 1
+print("sanitized replays", n)
+"""
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "sanitized replays 19" in r.stdout
