@@ -33,6 +33,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -2241,6 +2242,430 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
 #endif
 }
 
+// ================================================================================================
+// K = 1 trees: the fused simulation step as a chain kernel
+// ================================================================================================
+// With sampled_times = 1 every expansion creates exactly one child, so a tree is a chain: node i
+// sits at depth i, the leaf is the newest node and every selection walks the whole chain down to
+// the child the last expansion created (cnode.cpp:381-413 with one child per node).  Before the
+// fused launch of simulation s (hsx = s + 1) the tree holds nodes 0..hsx, the leaf is node hsx and
+// the back-propagation path is 0..hsx: every address a launch touches follows from its arguments,
+// so both waves issue all their loads at launch and only check the header when it arrives (a
+// graph replayed out of sequence falls back to the header's values).
+//
+// The work splits differently from k_step:
+//  - wave 1 computes only the bootstrap recurrence b_{i-1} = r_i + discount * b_i (cnode.cpp:
+//    424,448), the one serial chain of the step, and hands the values over through LDS;
+//  - wave 0 expands the leaf meanwhile (one draw), then updates every node of the chain
+//    (SubTreeValueSet::update appends to an empty depth class: utils.cpp:20-71 with count 0),
+//    recomputes the min/max normaliser over the chain's q values, and selects.  On a tame tree
+//    (select_walk's fast case) the selection is known without scoring: the new child, one engine
+//    word per level, and its parent's hidden_state_index_x is this launch's hsx.
+// One barrier per launch.  What K = 1 trees never read again is not written: value-set entries
+// (every update appends to an empty depth class), q of interior nodes (every back-propagation
+// recomputes all of them), maxdepth, parents, and the readback record D of non-root children.
+// --------------------------------------------------------------------------------------------
+template <int NC>  // node capacity class (P = S + 2 <= NC); 0: offsets from P at run time
+struct ChainLayout {
+    int oA, oC, oPP, oLp, oR, oBoot, oW, oP, total;
+    __host__ __device__ static constexpr int r16(int x) { return (x + 15) & ~15; }
+    __host__ __device__ constexpr ChainLayout(int P)
+        : oA(0),
+          oC(r16(16 * P)),
+          oPP(oC + r16(16 * P)),
+          oLp(oPP + r16(4 * P)),
+          oR(oLp + r16(4 * (P + 1 + kWave))),
+          oBoot(oR + r16(4 * (P + kWave))),
+          oW(oBoot + r16(4 * (P + kWave))),
+          oP(oW + r16(4 * kMaxActions)),
+          total(oP + r16(8 * kMaxActions)) {}
+};
+template <int NC>
+__device__ __forceinline__ ChainLayout<NC> chain_layout(int P) {
+    if constexpr (NC > 0) {
+        constexpr ChainLayout<NC> L(NC);
+        return L;
+    } else {
+        return ChainLayout<NC>(P);
+    }
+}
+int chain_lds_bytes(int P, int nc) { return ChainLayout<0>(nc > 0 ? nc : P).total; }
+
+// std::discrete_distribution's cumulative table (libstdc++ random.tcc:2656-2690, as cdf_lane) for
+// the weights bet (lane a < A): the sequential double sum and the sequential prefix sums run on
+// every lane from broadcast LDS reads (16 operands per batch of four 16-byte reads) instead of
+// v_readlane.  Trailing +0.0 terms of a batch are exact no-ops on the non-negative sums.  Lane a
+// returns cp[a] (cp[A-1] forced to 1.0).
+__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp) {
+    const int l = lane_id();
+    sw[l] = (l < A) ? bet : 0.f;  // kMaxActions = kWave entries
+    wait_lds();
+    double sum = 0.0;
+    for (int a0 = 0; a0 < A; a0 += 16) {
+        float w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = *(const float4 *)(sw + a0 + 4 * q);
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += (double)w[j];
+    }
+    const double p = (l < A) ? (double)bet / sum : 0.0;
+    sp[l] = p;
+    wait_lds();
+    double acc = 0.0, cp = 0.0;
+    for (int a0 = 0; a0 < A; a0 += 16) {
+        double pj[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
+            pj[2 * q] = v.x;
+            pj[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            acc = (a0 + j == 0) ? pj[0] : acc + pj[j];
+            cp = sel_lane(cp, acc, 1ull << (j & 63) << (a0 & 63));
+        }
+    }
+    if (l == A - 1) cp = 1.0;
+    return cp;
+}
+
+template <int NC>
+__global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA, int pk, const float *reward,
+                                               const float *value, const float *policy, const float *beta, int K,
+                                               int hsx, float discount, int fast_ok, const char *pool,
+                                               long long pool_stride, long long row_bytes, char *gather_out,
+                                               int *idx_x, int *idy, int *act) {
+    (void)pk;
+    (void)K;
+    const int B = BA & 0xffffff, A = (int)((unsigned)BA >> 24);
+    Dev d;
+    d.base = (gchar *)base;
+    arena_hot(d, B, P, PS);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const ChainLayout<NC> L = chain_layout<NC>(P);
+    unsigned char *sbig = smem + L.total;  // leaf rows above 4 KiB (LDS-DMA staging, 16 KiB)
+    int4 *sA = (int4 *)(smem + L.oA);
+    float4 *sC = (float4 *)(smem + L.oC);
+    float *sPP = (float *)(smem + L.oPP);
+    float *sLp = (float *)(smem + L.oLp);
+    float *sR = (float *)(smem + L.oR);
+    float *sBoot = (float *)(smem + L.oBoot);
+    const int t = blockIdx.x;
+    const int l = threadIdx.x & (kWave - 1);
+    const int wv = uni((int)(threadIdx.x >> 6));
+    const size_t nb = (size_t)t * P;
+    // ---- round 1: everything, from the arguments (the chain's length is hsx) ----
+    int Dp = hsx;  // back-propagation path 0..Dp, leaf Dp, tot = Dp + 1
+    if (Dp < 0 || Dp + 1 > P) Dp = 0;
+    float pol = 0.f, bet = 0.f;
+    unsigned long long st_old = 0;
+    long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
+    int4 leaf_b = make_int4(0, 0, 0, 0);
+    // the next leaf's parent is this launch's leaf (hidden_state_index_x = hsx): its row is
+    // fetched now and stored at the end (four 16-byte chunks per lane up to 4 KiB, LDS-DMA above)
+    const bool row_al = pool && (((row_bytes | pool_stride | (long long)(uintptr_t)pool |
+                                   (long long)(uintptr_t)gather_out) & 15) == 0);
+    const bool g_reg = row_al && row_bytes <= 4 * 16 * kWave;
+    const bool g_lds = row_al && !g_reg && row_bytes <= 16 * 16 * kWave;
+    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+    if (wv == 0) {
+        for (int i0 = 0; i0 <= Dp; i0 += kWave)
+            if (i0 + l <= Dp) {
+                glds16(d.A() + nb + i0 + l, sA + i0);
+                glds16(d.C() + nb + i0 + l, sC + i0);
+                glds4(d.PP() + nb + i0 + l, sPP + i0);
+                glds4(d.lp() + i0 + l, sLp + i0);
+            }
+        const size_t ib = (size_t)t * A;
+        if (l < A) {
+            pol = policy[ib + l];
+            bet = beta[ib + l];
+        }
+        if (l < MZ_S_CYC_HEADER) st_old = (unsigned long long)st[l];
+        leaf_b = d.Bn()[nb + Dp];
+        if (g_reg || g_lds) {
+            const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
+            const long long last = row_bytes - 16, o = (long long)l * 16;
+            if (g_reg) {
+                gv0 = *(const int4 *)(src + (o < last ? o : last));
+                gv1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
+                gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
+                gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) glds16(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+            }
+        }
+    } else {
+        for (int i0 = 0; i0 <= Dp; i0 += kWave)
+            if (i0 + l <= Dp) glds4(&d.A()[nb + i0 + l].w, sR + i0);
+    }
+    // the header, the leaf's structure record and the network outputs of this tree (scalar loads)
+    TreeHdr h;
+    {
+        const cTreeHdr *hp = (const cTreeHdr *)(d.hdr() + t);
+        h.cursor = hp->cursor;
+        h.tot = hp->tot;
+        h.D = hp->D;
+        h.err = hp->err;
+        h.tame = hp->tame;
+        h.leaf = hp->leaf;
+        h.nxt[0] = hp->nxt[0];
+        h.nxt[1] = hp->nxt[1];
+    }
+    const float r_in = reward[t], v_in = value[t];
+    const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
+    const int gW = pl->g.W;
+    const float omr = pl->g.one_minus_rho;
+    const unsigned oR = pl->d.o_R;
+    d.o_D = pl->d.o_D;
+    wait_vm();
+    if (h.err) {  // a dead tree stays dead (both waves see the same header)
+        if (wv == 0) {
+            if (l == 0) {
+                idx_x[t] = 0;
+                idy[t] = t;
+                act[t] = 0;
+            }
+        }
+        return;
+    }
+    // a graph replayed out of sequence: the header's chain, not the arguments' (both waves)
+    const int D = h.D;
+    if (D != Dp || h.tot != D + 1 || h.leaf != D) {
+        if (D + 1 > P || h.tot != D + 1 || h.leaf != D) {  // not a chain: refuse (reported below)
+            if (wv == 0 && l == 0) {
+                idx_x[t] = 0;
+                idy[t] = t;
+                act[t] = 0;
+                TreeHdr *hp = d.hdr() + t;
+                hp->err = kErrPath;
+                atomicOr(d.err(), kErrPath);
+            }
+            return;
+        }
+        for (int i0 = 0; i0 <= D; i0 += kWave)
+            if (i0 + l <= D) {
+                if (wv == 0) {
+                    glds16(d.A() + nb + i0 + l, sA + i0);
+                    glds16(d.C() + nb + i0 + l, sC + i0);
+                    glds4(d.PP() + nb + i0 + l, sPP + i0);
+                    glds4(d.lp() + i0 + l, sLp + i0);
+                } else {
+                    glds4(&d.A()[nb + i0 + l].w, sR + i0);
+                }
+            }
+        if (wv == 0) leaf_b = d.Bn()[nb + D];
+        wait_vm();
+    }
+
+    if (wv == 1) {
+        // ---- the bootstrap values b_i, i = D .. 0 (cnode.cpp:424,448), in chunks of 63 levels ----
+        float carry = v_in;
+        int hi = D;
+        const float dv = discount;
+        while (true) {
+            const int lo = hi > 63 ? hi - 63 : 0;
+            const int nl = hi - lo;
+            const int lev = hi - 63 + l;
+            float rn = 0.f;  // reward of the level above this lane's
+            if (lev >= lo && lev < hi) rn = (lev + 1 == D) ? r_in : sR[lev + 1];
+            float b = (l == 63) ? carry : 0.f;
+            float tmp = (l == 62) ? dv * carry : 0.f;
+            boot_dpp(b, tmp, dv, rn, nl);
+            if (lev >= lo && lev <= hi) sBoot[lev] = b;
+            if (lo == 0) break;
+            carry = rlf(b, 63 - nl);
+            hi = lo;
+        }
+        lds_barrier();
+        return;
+    }
+
+    // ---- wave 0: CTree::expand (cnode.cpp:224-295) of the leaf: one draw ----
+    int err = 0;
+    const int leaf = D, c = D + 1;  // the new child
+    int cursor = h.cursor;
+    int a = 0;
+    if (A >= 2) {
+        const double cp = cdf_bcast(bet, A, (float *)(smem + L.oW), (double *)(smem + L.oP));
+        const double w1 = (double)h.nxt[0], w2 = (double)h.nxt[1];
+        double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
+        if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+        a = __popcll(ballot(l < A && cp < u));    // lower_bound
+        cursor += 2;
+    }
+    a = uni(a);
+    if (c + 1 > P) err |= kErrPool;
+    const float bh = 1.0f;  // betahat_prob = count / sampled_times = 1 / 1
+    const float pol_a = rlf(pol, a), bet_a = rlf(bet, a);
+    float prior = pol_a * bh / bet_a;  // prior * betahat_prob / beta_prob (eps = 0 after the root)
+    const bool wild = !tame_prior(prior);
+    leaf_b = uni4(leaf_b);
+    if (!err && l == 0) {
+        const size_t gi = nb + c;
+        d.A()[gi] = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+        d.Bn()[gi] = make_int4(0, pack_y(0, a, -1), f2i(0.0f), -1);
+        d.C()[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d.PP()[gi] = v_in;
+        if (leaf == 0) d.D()[gi] = make_float4(pol_a, bet_a, bh, 0.f);  // (readbacks: root children)
+        const int md = md_of(leaf_b.y) < 0 ? 0 : md_of(leaf_b.y);
+        d.Bn()[nb + leaf] = make_int4(c, pack_y(1, act_of(leaf_b.y), md), f2i(v_in), hsx);
+    }
+    const int tame = (h.tame && !wild && tame_val(v_in) && tame_val(r_in)) ? 1 : 0;
+    const bool fast = fast_ok && tame && fabsf(discount) <= 1.0f;
+    // the selection on a tame tree (select_walk): the new child; one word per level but the
+    // forced first one (root visits after this back-propagation = the staged count + 1)
+    const int Ds = c;
+    int root_visit = 0, words = 0;
+    if (fast) {
+        root_visit = uni(sA[0].x) + 1;
+        if (root_visit - 1 >= PS) err |= kErrTable;
+        words = Ds - ((root_visit <= 1) ? 1 : 0);
+    }
+    if (Ds + 1 > PS) err |= kErrPath;
+    // the next expansion's engine words, for the header (in flight during the back-propagation)
+    unsigned nxt_w = 0;
+    const unsigned *Rt = (const unsigned *)(base + (size_t)oR * 256) + (size_t)t * gW;
+    if (fast && l < kNxt && cursor + words + l < gW) nxt_w = Rt[cursor + words + l];
+    if (value_lim(1, omr) != 1) err |= kErrValueSet;  // (count 1: size_lim must be 1, utils.cpp:31)
+
+    // ---- CTree::back_propagate (cnode.cpp:415-450) over the chain, lane i = node i ----
+    lds_barrier();  // the bootstrap values
+    float mn = INFINITY, mx = -INFINITY;
+    for (int i0 = 0; i0 <= D; i0 += kWave) {
+        const int i = i0 + l;
+        if (i <= D) {
+            const int dep = D - i;
+            const float key = sBoot[i];
+            int4 a4 = sA[i];
+            if (i == D) a4.w = f2i(r_in);  // the leaf's reward is this simulation's
+            const float4 cw = sC[i];
+            const float lp = sLp[dep];
+            float ws = cw.x, tw = cw.y;
+            tw += lp;  // an empty depth class: big gets the value (utils.cpp:36-44)
+            ws += lp * key;
+            const float val = ws / tw;  // CNode::value (cnode.cpp:42-56); every chain node has a child
+            const int4 na = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
+            sA[i] = na;
+            d.A()[nb + i] = na;
+            *(float2 *)&d.C()[nb + i] = make_float2(ws, tw);
+            if (i >= 1) {
+                const float q = (i2f(a4.w) + discount * val) - sPP[i];  // get_qsa - father->pred_value
+                mn = fminf(mn, q);
+                mx = fmaxf(mx, q);
+            }
+        }
+    }
+    // min / max over the q of the visited non-root nodes: the whole chain 1..D
+    mn = unif(rlf(wave_min_to63(mn), 63));
+    mx = unif(rlf(wave_max_to63(mx), 63));
+    const int mm_cnt = D;
+
+    if (!fast && !err) {
+        // ---- select_walk's exact case: every level's tie list must be non-empty to consume a
+        // word (score >= FLOAT_MIN, not NaN); levels 1..Ds scored in parallel ----
+        sA[c] = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+        wait_lds();
+        root_visit = uni(sA[0].x);
+        const float gdelta = pl->g.delta;
+        const bool mm_on = mm_cnt > 0;
+        float den = 0.f;
+        if (mm_on) {
+            const float delta = mx - mn;
+            den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
+        }
+        const float *pbt = d.pb();
+        const double *sqt = d.sq();
+        bool terr = false;
+        for (int i0 = 0; i0 <= Ds; i0 += kWave) {
+            const int i = i0 + l;
+            bool valid = false;
+            if (i >= 1 && i <= Ds && !(i == 1 && root_visit <= 1)) {
+                const int n = sA[i - 1].x - 1;  // the parent's total_children_visit_counts
+                if (n < 0 || n >= PS) {
+                    terr = true;
+                } else {
+                    const int4 ca = sA[i];
+                    const float pp = (i == Ds) ? v_in : sPP[i];
+                    float vs = (ca.x == 0) ? 0.0f : ((i2f(ca.w) + discount * i2f(ca.z)) - pp);
+                    if (mm_on) vs = (vs - mn) / den;
+                    if (vs < 0) vs = 0;
+                    if (vs > 1) vs = 1;
+                    const float pbc = (float)((double)pbt[n] * (sqt[n] / (double)(ca.x + 1)));
+                    const float sc = pbc * i2f(ca.y) + vs;
+                    valid = sc >= -1000000.0f;  // FLOAT_MIN (utils.h:12)
+                }
+            }
+            words += __popcll(ballot(valid));
+        }
+        if (ballot(terr)) err |= kErrTable;
+        if (!err && l < kNxt && cursor + words + l < gW) nxt_w = Rt[cursor + words + l];
+    }
+
+    // ---- outputs (mcts_sampled.py:123-134), the header, the statistics ----
+    if (l == 0) {
+        idx_x[t] = err ? 0 : hsx;  // parent->hidden_state_index_x: the expanded leaf's
+        idy[t] = t;
+        act[t] = err ? 0 : a;
+    }
+    if (pool && !err) {
+        const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
+        char *dst = gather_out + (long long)t * row_bytes;
+        const long long o = (long long)l * 16;
+        if (g_reg) {
+            if (o < row_bytes) *(int4 *)(dst + o) = gv0;
+            if (o + 1024 < row_bytes) *(int4 *)(dst + o + 1024) = gv1;
+            if (o + 2048 < row_bytes) *(int4 *)(dst + o + 2048) = gv2;
+            if (o + 3072 < row_bytes) *(int4 *)(dst + o + 3072) = gv3;
+        } else if (g_lds) {
+            for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(dst + o2) = *(const int4 *)(sbig + o2);
+        } else if (row_al) {
+            for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(dst + o2) = *(const int4 *)(src + o2);
+        } else {
+            for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
+                *(int *)(dst + o2) = *(const int *)(src + o2);
+        }
+    }
+    {
+        TreeHdr *hp = d.hdr() + t;
+        if (l < kNxt) hp->nxt[l] = nxt_w;
+        if (l == 0) {
+            hp->cursor = err ? h.cursor : cursor + words;
+            hp->tot = err ? h.tot : c + 1;
+            hp->D = err ? h.D : Ds;
+            hp->err = err;
+            hp->mm_min = mn;
+            hp->mm_max = mx;
+            hp->mm_cnt = mm_cnt;
+            hp->tame = tame;
+            hp->leaf = err ? h.leaf : c;
+        }
+    }
+    if (l < MZ_S_CYC_HEADER) {
+        long long add = 0;
+        switch (l) {
+            case MZ_S_SELECTS: add = 1; break;
+            case MZ_S_PATH_EDGES: add = Ds; break;
+            case MZ_S_SCORED: add = Ds; break;
+            case MZ_S_EXPANDS: add = 1; break;
+            case MZ_S_NEW_CHILDREN: add = 1; break;
+            case MZ_S_BACKUP_NODES: add = D + 1; break;
+            case MZ_S_MINMAX_NODES: add = D; break;
+            default: break;
+        }
+        st[l] = (long long)st_old + add;
+    }
+    if (l == 0 && err) atomicOr(d.err(), err);
+}
+
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
 // One device word, set by a kernel.  Captured search graphs never hold a runtime memset node: under
 // the HIP runtime's graph packet capture, a replayed hipMemsetAsync node can write a stale fill
@@ -2370,6 +2795,7 @@ struct mz_batch {
     bool prepared = false;
     long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
     int nc = 0;                // k_step layout class (0 = layout from Geo)
+    int chain_nc = -1;         // k_chain node class for K = 1 trees (-1: k_step for every launch)
     Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
 };
 
@@ -2389,6 +2815,11 @@ int fail(int code, const std::string &m) {
     } while (0)
 
 int round16(int x) { return (x + 15) & ~15; }
+
+bool getenv_flag(const char *name) {
+    const char *v = std::getenv(name);
+    return v && v[0] == '1';
+}
 
 const char *err_message(int bits) {
     if (bits & kErrValueSet) return "SubTreeValueSet::update: cur_size+1!=size_lim.";
@@ -2515,8 +2946,33 @@ void set_lds_limit(int lds) {
     (void)hipFuncSetAttribute((const void *)k_step<false, true, NC, JOINT>, attr, lds);
 }
 
+template <int NC>
+void launch_chain(mz_batch *b, const StepArgs &a, int lds) {
+    const Geo &g = b->geo;
+    hipLaunchKernelGGL((k_chain<NC>), dim3(g.B), dim3(2 * kWave), lds, b->stream, (char *)b->dev.base, g.P, g.PS,
+                       g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value, a.policy, a.beta, a.K, a.hsx,
+                       a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy,
+                       a.act);
+}
+
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
+    if (eb && sel && b->chain_nc >= 0) {  // K = 1 trees: the chain kernel
+        const bool big = a.pool && a.row_bytes > 4 * 16 * kWave && a.row_bytes <= 16 * 16 * kWave;
+        const int lds = chain_lds_bytes(g.P, b->chain_nc) + (big ? 16 * 16 * kWave : 0);
+        switch (b->chain_nc) {
+            case 64: launch_chain<64>(b, a, lds); break;
+            case 128: launch_chain<128>(b, a, lds); break;
+            case 256: launch_chain<256>(b, a, lds); break;
+            case 512: launch_chain<512>(b, a, lds); break;
+            case 1024: launch_chain<1024>(b, a, lds); break;
+            default: launch_chain<0>(b, a, lds); break;
+        }
+        HIP_TRY(hipGetLastError());
+        b->rb_valid = b->rb_dev_valid = false;
+        ++b->expansions;
+        return MZ_OK;
+    }
     // tot <= 1 + K * expansions and depth <= expansions: the kernel stages that much without
     // waiting for the tree header (and falls back to the header's values if they are larger)
     {
@@ -2729,6 +3185,15 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         delete b;
         return fail(MZ_ERR_UNSUPPORTED, "tree too large for the LDS-resident kernels (K*(S+2) nodes)");
     }
+    if (K == 1 && N == 1 && !getenv_flag("MZ_NO_CHAIN")) {
+        b->chain_nc = 0;
+        for (int nc : {64, 128, 256, 512, 1024})
+            if (b->P <= nc) {
+                b->chain_nc = nc;
+                break;
+            }
+        if (chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave > 160 * 1024) b->chain_nc = -1;
+    }
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
@@ -2805,6 +3270,20 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             case 512: set_lds_limit<512>(g.lds); break;
             case 1024: set_lds_limit<1024>(g.lds); break;
             default: set_lds_limit<0>(g.lds); break;
+        }
+    }
+    if (b->chain_nc >= 0) {
+        const int cl = chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave;
+        if (cl > 64 * 1024) {
+            const auto attr = hipFuncAttributeMaxDynamicSharedMemorySize;
+            switch (b->chain_nc) {
+                case 64: (void)hipFuncSetAttribute((const void *)k_chain<64>, attr, cl); break;
+                case 128: (void)hipFuncSetAttribute((const void *)k_chain<128>, attr, cl); break;
+                case 256: (void)hipFuncSetAttribute((const void *)k_chain<256>, attr, cl); break;
+                case 512: (void)hipFuncSetAttribute((const void *)k_chain<512>, attr, cl); break;
+                case 1024: (void)hipFuncSetAttribute((const void *)k_chain<1024>, attr, cl); break;
+                default: (void)hipFuncSetAttribute((const void *)k_chain<0>, attr, cl); break;
+            }
         }
     }
     *out = b;
