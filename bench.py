@@ -249,7 +249,8 @@ class HipLeg:
         achieved = bytes_per_launch / avg / 1e9
         pmc = pmc_traffic(self.args)
         r = dict(
-            kernel="k_step<true,true> (fused expand+backup+select+gather)",
+            kernel=("k_chain (K = 1 fused expand+backup+select+gather)" if K == 1 else
+                    "k_step<true,true> (fused expand+backup+select+gather)"),
             bound="hbm",
             achieved=round(achieved, 3),
             peak=8000.0,

@@ -289,6 +289,20 @@ __device__ __forceinline__ void glds16(const void *src, void *lds_base) {
     __builtin_amdgcn_global_load_lds((glb_void *)src, (lds_void *)lds_base, 16, 0, 0);
 }
 
+// The same LDS-DMA issued through inline assembly: the compiler's wait-count pass does not track it,
+// so it inserts no conservative vmcnt(0) before later LDS accesses (with the builtin, any LDS access
+// after a DMA on ANY control-flow path -- another wave's role branch included -- waits for every
+// outstanding vector memory operation, this wave's global stores too).  The caller waits (wait_vm)
+// before it reads the staged data.
+__device__ __forceinline__ void glds4a(const void *src, void *lds_base) {
+    const unsigned lds = (unsigned)(uintptr_t)(lds_void *)lds_base;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+__device__ __forceinline__ void glds16a(const void *src, void *lds_base) {
+    const unsigned lds = (unsigned)(uintptr_t)(lds_void *)lds_base;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
 // Phase stamp (diagnostic builds): the shader clock when the wave's instruction stream gets here
 // (no forced wait: loads in flight stay in flight).
 __device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
@@ -928,6 +942,7 @@ __device__ __forceinline__ void boot_dpp(float &b, float &tmp, float dv, float r
 // chains).  Chunks hold <= 64 nodes whose needed entries fit g.reg_cap.  Returns cnt (uniform);
 // lane l gets its node id, entry count (= visit at selection), need flag and staging offset.
 // --------------------------------------------------------------------------------------------
+template <bool kAsmDma = false>
 __device__ __forceinline__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &need,
                              int &off) {
     const int l = lane_id();
@@ -972,7 +987,10 @@ __device__ __forceinline__ int stage_regions(const Geo &g, const Dev &d, Lds &s,
         const int dw = 2 * vj;
         const int *src = (const int *)(gV + (size_t)nj * g.E);
         for (int c = 0; c < dw; c += kWave)
-            if (c + l < dw) glds4(src + c + l, regdw + 2 * oj + c);
+            if (c + l < dw) {
+                if constexpr (kAsmDma) glds4a(src + c + l, regdw + 2 * oj + c);
+                else glds4(src + c + l, regdw + 2 * oj + c);
+            }
     }
     return cnt;
 }
@@ -2336,6 +2354,50 @@ __device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double 
     return cp;
 }
 
+// A wave-uniform load through the scalar cache (s_load: counted by lgkmcnt, not vmcnt)
+__device__ __forceinline__ float ldsc(const float *p) {
+    return *(const __attribute__((address_space(4))) float *)p;
+}
+
+// cdf_bcast for weights already staged in sw[0..A) (sw[l] = 0 for l >= A)
+__device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp) {
+    const int l = lane_id();
+    double sum = 0.0;
+    for (int a0 = 0; a0 < A; a0 += 16) {
+        float w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = *(const float4 *)(sw + a0 + 4 * q);
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += (double)w[j];
+    }
+    const double p = (l < A) ? (double)sw[l] / sum : 0.0;
+    sp[l] = p;
+    wait_lds();
+    double acc = 0.0, cp = 0.0;
+    for (int a0 = 0; a0 < A; a0 += 16) {
+        double pj[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
+            pj[2 * q] = v.x;
+            pj[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            acc = (a0 + j == 0) ? pj[0] : acc + pj[j];
+            cp = sel_lane(cp, acc, 1ull << (j & 63) << (a0 & 63));
+        }
+    }
+    if (l == A - 1) cp = 1.0;
+    return cp;
+}
+
 template <int NC>
 __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA, int pk, const float *reward,
                                                const float *value, const float *policy, const float *beta, int K,
@@ -2666,6 +2728,1020 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     if (l == 0 && err) atomicOr(d.err(), err);
 }
 
+// ================================================================================================
+// General trees (2 <= sampled_times <= 64, agent_num = 1, pools of <= 1024 nodes): the fused
+// simulation step on four waves
+// ================================================================================================
+// k_step's general walks score every node (or build every internal node's tie list) after the
+// back-propagation, on one wave's critical path.  Here the work is split by what it depends on:
+//  - the back-propagation changes only the path nodes (visits + 1, value, the leaf's reward) and
+//    the min/max normaliser.  The prior part of every ucb score, pb_c(parent's child visits, child
+//    visits) * prior (cnode.cpp:313-316), is therefore known before the back-propagation ends:
+//    visits after it are the staged ones plus one on the path.  Waves 2 and 3 compute it for every
+//    node (pb_c from the host-built table in HBM, one gather per node), and the min/max over the
+//    visited nodes off the path, while wave 1 back-propagates and wave 0 expands the leaf;
+//  - after the barrier that hands the results over, wave 0 joins the min/max with the path nodes'
+//    new q values and walks level by level (select_child, cnode.cpp:337-379): per level only the
+//    value scores of the node's children (one lane each) are computed, from records read in one
+//    LDS round trip that also carries the next level's structure record.
+// Two barriers: after round 1 (every staged record has landed, path nodes flagged) and after the
+// expansion / back-propagation / prior scores.  The engine-word draws of the expansion need no
+// staged record and run before the first.
+// --------------------------------------------------------------------------------------------
+template <int NC>
+struct TreeLayout {
+    static constexpr int r16(int x) { return (x + 15) & ~15; }
+    static constexpr int PSx = NC / 2 + 1;                         // PS = S + 2 <= P / K <= NC / 2
+    static constexpr int oA = 0;                                   // int4 [NC] staged {visit, prior, value, reward}
+    static constexpr int oB = oA + r16(16 * NC);                   // int4 [NC] staged structure records
+    static constexpr int oPP = oB + r16(16 * NC);                  // f32 [NC] parent's pred_value
+    static constexpr int oQ = oPP + r16(4 * NC);                   // f32 [NC] min/max members
+    static constexpr int oPar = oQ + r16(4 * NC);                  // i32 [NC] parent index
+    static constexpr int oPS = oPar + r16(4 * NC);                 // f32 [NC] prior score after the back-propagation
+    static constexpr int oFl = oPS + r16(4 * NC);                  // i32 [NC] 1 + path level (path nodes), else 0
+    static constexpr int oAz = oFl + r16(4 * NC);                  // float2 [NC] path nodes' new {value, reward}
+    static constexpr int oPath = oAz + r16(8 * NC);                // int2 [PSx] the path {node, visits at selection}
+    static constexpr int oCw = oPath + r16(8 * (PSx + kWave));     // float4 [PSx] path nodes' value-set scalars
+    static constexpr int oLp = oCw + r16(16 * (PSx + kWave));      // f32 lambda powers
+    static constexpr int oRng = oLp + r16(4 * (PSx + 1 + kWave));  // u32 [kRngWin] engine words
+    static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 bootstrap values
+    static constexpr int oReg = oBoot + r16(4 * (PSx + kWave));    // int2 [kRegCap] value entries; big leaf rows
+    static constexpr int oX = oReg + r16(8 * kRegCap);             // exchange between the waves
+    static constexpr int oW = oX + r16(256);                       // f32 [64] sampling weights
+    static constexpr int oP = oW + r16(4 * kWave);                 // f64 [64] probabilities, then the CDF
+    static constexpr int oU = oP + r16(8 * kWave);                 // f64 [64] the draws' canonical doubles
+    static constexpr int oIx = oU + r16(8 * kWave);                // i32 [64] the draws' actions
+    static constexpr int oPol = oIx + r16(4 * kWave);              // f32 [64] the leaf's policy
+    static constexpr int oNxt = oPol + r16(4 * kWave);             // u32 [64] the header's engine words
+    static constexpr int oSt = oNxt + r16(4 * kWave);              // i64 [64] the tree's statistics counters
+    static constexpr int total = oSt + r16(8 * kWave);
+};
+int tree_lds_bytes(int nc) {
+    switch (nc) {
+        case 64: return TreeLayout<64>::total;
+        case 128: return TreeLayout<128>::total;
+        case 256: return TreeLayout<256>::total;
+        case 384: return TreeLayout<384>::total;
+        case 512: return TreeLayout<512>::total;
+        default: return TreeLayout<1024>::total;
+    }
+}
+
+// CTree::back_propagate (cnode.cpp:415-450) for k_tree: backup()'s arithmetic and value-entry
+// updates, but the staged node records stay as they were (the prior-score waves read them): the
+// path nodes' new {value, reward} go to sAz, their q values into this wave's min / max, the rest to
+// HBM.  Path level i's value-set scalars are sCw[i].
+__device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, const float4 *sCw, float2 *sAz, int t,
+                                            int D, float value, float reward, float disc, int cnt0, int n0, int nv0,
+                                            int need0, int off0, int &err, long long &ent_r, long long &ent_w,
+                                            float &pmn, float &pmx, unsigned long long *tb) {
+    const int l = lane_id();
+    {  // bootstrap values b_{i-1} = reward_i + discount * b_i (cnode.cpp:424,448), as backup()
+        float carry = value;
+        int hi = D;
+        while (true) {
+            const int lo = hi > 63 ? hi - 63 : 0;
+            const int nl = hi - lo;
+            const int lev = hi - 63 + l;
+            float rn = 0.f;
+            if (lev >= lo && lev < hi) rn = (lev + 1 == D) ? reward : i2f(s.A[s.path[lev + 1].x].w);
+            float b = (l == 63) ? carry : 0.f;
+            float tmp = (l == 62) ? disc * carry : 0.f;
+            boot_dpp(b, tmp, disc, rn, nl);
+            if (lev >= lo && lev <= hi) s.boot[lev] = b;
+            if (lo == 0) break;
+            carry = rlf(b, 63 - nl);
+            hi = lo;
+        }
+    }
+    if (MZ_STAMPS) {
+        wait_lds();
+        stamp(tb, 1);
+    }
+    int2 *gV = d.V() + (size_t)t * g.P * g.E;
+    int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0;
+    pmn = INFINITY;
+    pmx = -INFINITY;
+    for (int i0 = 0; i0 <= D;) {
+        if (cnt == 0) {
+            err |= kErrPath;
+            return;
+        }
+        wait_vm();
+        wait_lds();
+        if (MZ_STAMPS && i0 == 0) stamp(tb, 2);
+        const int i = i0 + l;
+        int lo = nv, c = 0, pv = 0;  // entries of a smaller depth / the same depth / same depth, smaller value
+        const float key = (l < cnt) ? s.boot[i] : 0.f;
+        for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
+            const int j = __builtin_ctzll(m);
+            const int nvj = rl(nv, j), offj = rl(off, j), depj = D - (i0 + j);
+            const float keyj = rlf(key, j);
+            int cl = 0, cc = 0, cp = 0;
+            for (int e0 = 0; e0 < nvj; e0 += kWave) {
+                const bool on = e0 + l < nvj;
+                const int2 e = on ? s.reg[offj + e0 + l] : make_int2(0x7fffffff, 0);
+                cl += __popcll(ballot(on && e.x < depj));
+                cc += __popcll(ballot(on && e.x == depj));
+                cp += __popcll(ballot(on && e.x == depj && i2f(e.y) < keyj));
+            }
+            if (l == j) {
+                lo = cl;
+                c = cc;
+                pv = cp;
+            }
+            ent_r += nvj;
+        }
+        int pos = 0;
+        if (l < cnt) {
+            const int dep = D - i;
+            const int2 *R = s.reg + off;
+            const float4 cw = sCw[i];
+            float ws = cw.x, tw = cw.y;
+            const float lp = s.lp[dep];
+            const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
+            const int nl = value_lim(c + 1, g.one_minus_rho);
+            if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
+                const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
+                if (!(key < mb)) {
+                    ws -= lp * mb;
+                    tw -= lp;
+                    tw += lp;
+                    ws += lp * key;
+                }
+            } else {
+                if (cur + 1 != nl) err |= kErrValueSet;
+                if (c - cur == 0) {
+                    tw += lp;
+                    ws += lp * key;
+                } else {
+                    const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
+                    if (key > ms) {
+                        tw += lp;
+                        ws += lp * key;
+                    } else {
+                        tw += lp;
+                        ws += lp * ms;
+                    }
+                }
+            }
+            pos = lo + pv;
+            int2 *G = gV + (size_t)n * g.E;
+            if (nv + 1 > g.E) {
+                err |= kErrPath;
+                pos = nv;
+            } else {
+                G[pos] = make_int2(dep, f2i(key));
+            }
+            const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
+            int4 a4 = s.A[n];
+            if (is_leaf) a4.w = f2i(reward);
+            const int4 b4 = s.B[n];
+            const int nc = is_leaf ? 1 : nc_of(b4.y);
+            const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
+            const size_t gi = (size_t)t * g.P + n;
+            d.A()[gi] = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
+            d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
+            if (!is_leaf && dep > md_of(b4.y)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
+            sAz[n] = make_float2(val, i2f(a4.w));
+            if (i >= 1) {
+                const float q = (i2f(a4.w) + disc * val) - s.PP[n];  // get_qsa - father->pred_value
+                d.Q()[gi] = q;
+                pmn = fminf(pmn, q);
+                pmx = fmaxf(pmx, q);
+            }
+        }
+        for (unsigned long long m = ballot(l < cnt && nv > pos); m; m &= m - 1ull) {  // tails up by one
+            const int j = __builtin_ctzll(m);
+            const int nvj = rl(nv, j), posj = rl(pos, j), offj = rl(off, j), nj = rl(n, j);
+            ent_w += nvj - posj;
+            int2 *Gj = gV + (size_t)nj * g.E;
+            for (int e0 = posj; e0 < nvj; e0 += kWave)
+                if (e0 + l < nvj) Gj[e0 + l + 1] = s.reg[offj + e0 + l];
+        }
+        ent_w += cnt;
+        wait_lds();
+        i0 += cnt;
+        if (i0 <= D) cnt = stage_regions<true>(g, d, s, t, D, i0, n, nv, need, off);
+    }
+    if (MZ_STAMPS) {
+        wait_lds();
+        stamp(tb, 3);
+    }
+}
+
+// k_tree after barrier (2), run by all four waves (64-node blocks dealt round-robin):
+//  (S1) every node's ucb score under its parent (cnode.cpp:297-335) -- the prior score of waves 2
+//       and 3 plus the value score, min/max-normalised with the joined min/max -- in place of the
+//       prior score;
+//  (S2) every node's select_child outcome (cnode.cpp:337-379): the reference's sequential arg-max
+//       with epsilon ties over its children's scores.  A one-child tie list (the usual case) is
+//       stored as the next node (sPar, free now); leaves get kTreeLeaf; other lists (ties, an empty
+//       list, a parent beyond the pUCT table) get kTreeSlow and an exact record: list bits in sAz,
+//       size | table error << 16 in sQ.
+// Wave 0 then chases next nodes one LDS read per level.
+constexpr int kTreeLeaf = -1, kTreeSlow = -2;
+
+// The 1024-node class walks level by level instead (O(depth) after the barrier instead of
+// O(pool) / 4 waves).  Measured on one box, k_tree fused launch: 27m K = 5 (1010 nodes) 13.8 us by
+// levels against 14.1 us with tree_select_prep; 3m K = 5 (260 nodes) 10.4 against 11.6 us,
+// 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
+template <int NC>
+constexpr bool kTreeLevels = (NC >= 1024);
+
+template <int NC>
+__device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
+                                                 int D, unsigned long long *tp = nullptr) {
+    using L = TreeLayout<NC>;
+    const int l = lane_id();
+    const int4 *sA = (const int4 *)(smem + L::oA);
+    const int4 *sB = (const int4 *)(smem + L::oB);
+    const float *sPP = (const float *)(smem + L::oPP);
+    float *sQ = (float *)(smem + L::oQ);
+    int *nxt = (int *)(smem + L::oPar);
+    float *sSc = (float *)(smem + L::oPS);
+    const int *sFl = (const int *)(smem + L::oFl);
+    float2 *sAz = (float2 *)(smem + L::oAz);
+    const float *xf = (const float *)(smem + L::oX);
+    const int *xi = (const int *)(smem + L::oX);
+    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), unif(xf[4]));
+    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), unif(xf[5]));
+    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
+    const bool mm_on = mm_cnt > 0;
+    float den = 0.f;
+    if (mm_on) {
+        const float delta = mmx - mmn;
+        den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
+    }
+    for (int n0 = wv * kWave; n0 < ntot; n0 += 4 * kWave) {  // (S1)
+        const int n = n0 + l;
+        if (n >= 1 && n < ntot) {
+            const int4 a = sA[n];
+            const int fl = sFl[n];
+            const float2 az = sAz[n];
+            const int vis = a.x + (fl ? 1 : 0);
+            const float val = fl ? az.x : i2f(a.z);
+            const float rw = fl ? az.y : i2f(a.w);
+            float vs = (vis == 0) ? 0.0f : ((rw + disc * val) - sPP[n]);
+            if (mm_on) vs = (vs - mmn) / den;
+            if (vs < 0) vs = 0;
+            if (vs > 1) vs = 1;
+            sSc[n] = sSc[n] + vs;  // prior_score + value_score
+        }
+    }
+    if (MZ_STAMPS && tp) {
+        wait_lds();
+        tp[0] = __builtin_amdgcn_s_memtime();
+    }
+    lds_barrier();  // (3)
+    for (int p0 = wv * kWave; p0 < ntot; p0 += 4 * kWave) {  // (S2)
+        const int p = p0 + l;
+        if (p < ntot) {
+            const int4 b = sB[p];
+            const int fc = b.x, nc = nc_of(b.y);
+            if (nc == 0) {
+                nxt[p] = kTreeLeaf;
+            } else {
+                const int np = sA[p].x + (sFl[p] ? 1 : 0) - 1;  // total_children_visit_counts
+                const bool terr = np < 0 || np >= PS;
+                float mx = -1000000.0f;  // FLOAT_MIN (utils.h:12)
+                unsigned long long lst = 0ull;
+                int cnt = 0;
+                for (int i0 = 0; i0 < nc; i0 += 4) {
+                    float sc[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) sc[u] = sSc[fc + ((i0 + u < nc) ? i0 + u : i0)];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int i = i0 + u;
+                        const float v = sc[u];
+                        const bool ok = i < nc;
+                        const bool gt = ok && (mx < v);
+                        const bool ge = ok && !gt && (v >= mx - 0.000001f);
+                        const unsigned long long bit = 1ull << (i & 63);
+                        lst = gt ? bit : (ge ? (lst | bit) : lst);
+                        cnt = gt ? 1 : (cnt + (ge ? 1 : 0));
+                        mx = gt ? v : mx;
+                    }
+                }
+                if (cnt == 1 && !terr) {
+                    nxt[p] = fc + __builtin_ctzll(lst);
+                } else {
+                    nxt[p] = kTreeSlow;
+                    sAz[p] = make_float2(i2f((int)(unsigned)(lst & 0xffffffffull)), i2f((int)(unsigned)(lst >> 32)));
+                    sQ[p] = i2f(cnt | (terr ? 0x10000 : 0));
+                }
+            }
+        }
+    }
+    if (MZ_STAMPS && tp) {
+        wait_lds();
+        tp[1] = __builtin_amdgcn_s_memtime();
+    }
+    lds_barrier();  // (4)
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA, int pk, const float *reward,
+                                              const float *value, const float *policy, const float *beta, int K,
+                                              int hsx, float discount, int fast_ok, const char *pool,
+                                              long long pool_stride, long long row_bytes, char *gather_out,
+                                              int *idx_x, int *idy, int *act) {
+    // Each wave role runs to its own return: no control-flow join follows the split, so the
+    // compiler's wait-count state of one role (its loads, stores and LDS-DMA) never forces waits
+    // into another's code.  The barriers are the same two s_barrier in every role.
+    using L = TreeLayout<NC>;
+    (void)fast_ok;
+    const int B = BA & 0xffffff, A = (int)((unsigned)BA >> 24);
+    const int pe = pk & 0x1ffff, gK = (int)((unsigned)pk >> 17);
+    const int ne = (1ll + (long long)gK * (pe - 1)) < P ? 1 + gK * (pe - 1) : P;  // node bound (launch_step)
+    Dev d;
+    d.base = (gchar *)base;
+    arena_hot(d, B, P, PS);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int4 *sA = (int4 *)(smem + L::oA);
+    int4 *sB = (int4 *)(smem + L::oB);
+    float *sPP = (float *)(smem + L::oPP);
+    float *sQ = (float *)(smem + L::oQ);
+    int *sPar = (int *)(smem + L::oPar);
+    float *sPS = (float *)(smem + L::oPS);
+    int *sFl = (int *)(smem + L::oFl);
+    float2 *sAz = (float2 *)(smem + L::oAz);
+    int2 *sPath = (int2 *)(smem + L::oPath);
+    float4 *sCw = (float4 *)(smem + L::oCw);
+    float *sLp = (float *)(smem + L::oLp);
+    unsigned *sRng = (unsigned *)(smem + L::oRng);
+    float *xf = (float *)(smem + L::oX);
+    int *xi = (int *)(smem + L::oX);
+    long long *xl = (long long *)(smem + L::oX + 64);
+    const int t = blockIdx.x;
+    const int l = threadIdx.x & (kWave - 1);
+    const int wv = uni((int)(threadIdx.x >> 6));
+    const size_t nb = (size_t)t * P;
+    unsigned long long ts[10] = {0};
+    stamp(ts, 0);
+    const cTreeHdr *hp0 = (const cTreeHdr *)(d.hdr() + t);
+    const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
+
+    if (wv == 2 || wv == 3) {
+        // ======== waves 2, 3: stage the node records; then the prior scores after the
+        // back-propagation and the min/max over the visited nodes off the path ========
+        for (int i0 = 0; i0 < ne; i0 += kWave)
+            if (i0 + l < ne) {
+                if (wv == 2) {
+                    glds16a(d.A() + nb + i0 + l, sA + i0);
+                    glds16a(d.Bn() + nb + i0 + l, sB + i0);
+                } else {
+                    glds4a(d.PP() + nb + i0 + l, sPP + i0);
+                    glds4a(d.Q() + nb + i0 + l, sQ + i0);
+                    glds4a(d.Par() + nb + i0 + l, sPar + i0);
+                }
+            }
+        const int herr = hp0->err, tot = hp0->tot;
+        if (herr) {
+            wait_vm();
+            return;
+        }
+        if (tot > ne)  // slow path: the host bound was too small (a graph replayed out of sequence)
+            for (int i0 = ne; i0 < tot; i0 += kWave)
+                if (i0 + l < tot) {
+                    if (wv == 2) {
+                        glds16a(d.A() + nb + i0 + l, sA + i0);
+                        glds16a(d.Bn() + nb + i0 + l, sB + i0);
+                    } else {
+                        glds4a(d.PP() + nb + i0 + l, sPP + i0);
+                        glds4a(d.Q() + nb + i0 + l, sQ + i0);
+                        glds4a(d.Par() + nb + i0 + l, sPar + i0);
+                    }
+                }
+        wait_vm();
+        lds_barrier();  // (1)
+        // nodes 1 .. tot-1 in 64-node blocks, alternating between the two waves
+        constexpr int NBW = (NC + 2 * kWave - 1) / (2 * kWave);
+        const float *T = d.T();
+        float pbc[NBW];
+        float mn = INFINITY, mx = -INFINITY;
+        int cv = 0;
+#pragma unroll
+        for (int k = 0; k < NBW; ++k) {
+            const int n = (2 * k + wv - 2) * kWave + l;
+            pbc[k] = 0.f;
+            if (n >= 1 && n < tot) {
+                const int4 a = sA[n];
+                const int p = sPar[n];
+                const int np = sA[p].x + (sFl[p] ? 1 : 0) - 1;  // the parent's total child visits, after
+                const int fn = sFl[n];
+                int v = a.x + (fn ? 1 : 0);
+                if (np >= 0 && np < PS) {
+                    if (v > np) v = np;  // (not in a consistent tree; keeps the read in range)
+                    pbc[k] = T[np * (np + 1) / 2 + v];
+                }
+                if (a.x > 0 && !fn) {
+                    const float q = sQ[n];
+                    mn = fminf(mn, q);
+                    mx = fmaxf(mx, q);
+                    ++cv;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NBW; ++k) {
+            const int n = (2 * k + wv - 2) * kWave + l;
+            if (n >= 1 && n < tot) sPS[n] = pbc[k] * i2f(sA[n].y);  // pb_c * prior (cnode.cpp:316)
+        }
+        cv = wave_sum(cv);
+        mn = wave_min_to63(mn);
+        mx = wave_max_to63(mx);
+        if (l == 63) {
+            xf[2 * (wv - 1)] = mn;
+            xf[2 * (wv - 1) + 1] = mx;
+        }
+        if (l == 0) xi[7 + wv] = cv;
+        lds_barrier();  // (2)
+        if constexpr (!kTreeLevels<NC>) {
+            const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[14]);
+            tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, pl->g.delta, PS, hp0->D);
+        }
+        return;
+    }
+
+    if (wv == 1) {
+        // ======== wave 1: the path; then CTree::back_propagate (cnode.cpp:415-450) ========
+        for (int i0 = 0; i0 < 2 * pe; i0 += kWave)
+            if (i0 + l < 2 * pe) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
+        for (int i0 = 0; i0 < PS + 1; i0 += kWave)
+            if (i0 + l < PS + 1) glds4a(d.lp() + i0 + l, sLp + i0);
+        const int herr = hp0->err, tot = hp0->tot, D = hp0->D;
+        const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
+        Geo g;
+        g.B = B;
+        g.A = A;
+        g.K = gK;
+        g.P = P;
+        g.PS = PS;
+        g.E = pl->g.E;
+        g.one_minus_rho = pl->g.one_minus_rho;
+        g.reg_cap = pl->g.reg_cap;
+        d.o_V = pl->d.o_V;
+        if (herr) {
+            wait_vm();
+            return;
+        }
+        if (D + 1 > pe)
+            for (int i0 = 2 * pe; i0 < 2 * (D + 1); i0 += kWave)
+                if (i0 + l < 2 * (D + 1)) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
+        const int nf = tot > ne ? tot : ne;  // path-node flags: cleared, then set once the path landed
+        for (int i0 = 0; i0 < nf; i0 += kWave)
+            if (i0 + l < nf) sFl[i0 + l] = 0;
+        wait_vm();
+        for (int i0 = 0; i0 <= D; i0 += kWave)
+            if (i0 + l <= D) {
+                const int n = sPath[i0 + l].x;
+                if (n >= 0 && n < tot) sFl[n] = i0 + l + 1;
+            }
+        lds_barrier();  // (1)
+        stamp(ts, 1);
+        // the path nodes' value-set scalars, then the value entries the updates need
+        // (stage_regions), the bootstrap chain meanwhile
+        for (int i0 = 0; i0 <= D; i0 += kWave)
+            if (i0 + l <= D) {
+                const int n = sPath[i0 + l].x;
+                glds16a(d.C() + nb + ((n >= 0 && n < tot) ? n : 0), sCw + i0);
+            }
+        Lds s{};
+        s.A = sA;
+        s.B = sB;
+        s.PP = sPP;
+        s.path = sPath;
+        s.lp = sLp;
+        s.boot = (float *)(smem + L::oBoot);
+        s.reg = (int2 *)(smem + L::oReg);
+        int n0 = 0, nv0 = 0, need0 = 0, off0 = 0;
+        int err = 0;
+        const int cnt0 = stage_regions<true>(g, d, s, t, D, 0, n0, nv0, need0, off0);
+        long long ent_r = 0, ent_w = 0;
+        float pmn, pmx;
+        unsigned long long tb[5] = {0};
+        stamp(tb, 0);
+        backup_tree(g, d, s, sCw, sAz, t, D, v_in, r_in, discount, cnt0, n0, nv0, need0, off0, err, ent_r, ent_w, pmn,
+                    pmx, tb);
+        pmn = wave_min_to63(pmn);
+        pmx = wave_max_to63(pmx);
+        if (l == 63) {
+            xf[0] = pmn;
+            xf[1] = pmx;
+        }
+        if (l == 0) {
+            xi[8] = err;
+            xl[0] = ent_r;
+            xl[1] = ent_w;
+            if (MZ_STAMPS) {
+                xl[2] = (long long)(__builtin_amdgcn_s_memtime() - ts[1]);
+                xl[3] = (long long)(tb[0] - ts[1]);
+                xl[4] = (long long)(tb[1] - tb[0]);
+                xl[5] = (long long)(tb[2] - tb[1]);
+                xl[6] = (long long)(tb[3] - tb[2]);
+            }
+        }
+        lds_barrier();  // (2): its global stores stay in flight
+        if constexpr (!kTreeLevels<NC>) {
+            const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[14]);
+            tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, pl->g.delta, PS, D);
+        }
+        wait_vm();  // nothing of this wave may be in flight when the block ends
+        return;
+    }
+
+    // ======== wave 0: expansion (cnode.cpp:224-295), selection (381-413), gather, header ========
+    // Round 1 is LDS-DMA and scalar loads only, so every wait below is an explicit, counted one:
+    // the four window chunks may stay in flight through the draws.
+    const bool have_w = 2 * K <= kNxt;  // the expansion's words are in the header
+    float *sW = (float *)(smem + L::oW);
+    float *sPol = (float *)(smem + L::oPol);
+    unsigned *sNxt = (unsigned *)(smem + L::oNxt);
+    long long *sSt = (long long *)(smem + L::oSt);
+    long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
+    constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
+    {
+        const size_t ib = (size_t)t * A + (l < A ? l : 0);
+        glds4a(policy + ib, sPol);
+        glds4a(beta + ib, sW);  // (lanes >= A: zero weights, below)
+        glds4a(&d.hdr()[t].nxt[l < kNxt ? l : 0], sNxt);
+        glds4a((const int *)st + (l < 2 * MZ_S_COUNT ? l : 0), (int *)sSt);
+    }
+    const float t00 = ldsc(d.T());  // pb_c(0, 0): the coefficient of the leaf's new children
+    TreeHdr h;
+    h.cursor = hp0->cursor;
+    h.tot = hp0->tot;
+    h.D = hp0->D;
+    h.err = hp0->err;
+    h.tame = hp0->tame;
+    h.leaf = hp0->leaf;
+    const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
+    const int gW = pl->g.W;
+    const float gdelta = pl->g.delta;
+    d.o_D = pl->d.o_D;
+    d.o_R = pl->d.o_R;
+    const int wbase = h.cursor;
+    {  // the selection's engine words (the expansion's when K > kNxt / 2): always four chunks
+        const unsigned *Rt = d.R() + (size_t)t * gW;
+#pragma unroll
+        for (int i0 = 0; i0 < kRngWin; i0 += kWave) {
+            const int w = wbase + i0 + l;
+            glds4a(Rt + (w < gW ? w : gW - 1), sRng + i0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // round 1 landed (the window may not have)
+    unsigned long long tq[4] = {0};
+    stamp(tq, 0);
+    if (h.err) {  // a dead tree stays dead (every wave reads the same header)
+        if (l == 0) {
+            idx_x[t] = 0;
+            idy[t] = t;
+            act[t] = 0;
+        }
+        wait_vm();
+        return;
+    }
+    const int tot = h.tot, D = h.D;
+    if (l >= A) sW[l] = 0.f;
+    const float pol = sPol[l < A ? l : 0], bet = sW[l < A ? l : 0];
+    stamp(ts, 1);
+    // (1) every staged record has landed and the path nodes are flagged: wave 1 back-propagates and
+    // waves 2, 3 score from here on, while this wave expands
+    lds_barrier();
+    stamp(ts, 2);
+    // the sampling distribution and the K draws (std::discrete_distribution, two engine words per
+    // draw, cnode.cpp:243-262)
+    int cursor = h.cursor;
+    int cnt = 0;  // draws that hit action l
+    int err = 0;
+    if (A < 2) {
+        cnt = (l == 0) ? K : 0;
+    } else {
+        double *sp = (double *)(smem + L::oP);
+        double *su = (double *)(smem + L::oU);
+        int *six = (int *)(smem + L::oIx);
+        wait_lds();
+        const double cp = cdf_staged(A, sW, sp);
+        if (MZ_STAMPS) {
+            asm volatile("" ::"v"(cp));
+            stamp(tq, 1);
+        }
+        if (!have_w) wait_vm();  // the words come from the window
+        double u = 0.0;
+        if (l < K) {
+            const unsigned a1 = have_w ? sNxt[2 * l] : ((2 * l < kRngWin) ? sRng[2 * l] : 0u);
+            const unsigned a2 = have_w ? sNxt[2 * l + 1] : ((2 * l + 1 < kRngWin) ? sRng[2 * l + 1] : 0u);
+            u = ((double)a1 + (double)a2 * 4294967296.0) / 18446744073709551616.0;
+            if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+        }
+        if (cursor + 2 * K > gW || 2 * K > kRngWin) err |= kErrRng;
+        sp[l] = cp;
+        su[l] = u;
+        wait_lds();
+        // lower_bound of draw k (lane k): the actions whose cumulative probability is below u_k
+        int ix = 0;
+        for (int a0 = 0; a0 < A; a0 += 8) {
+            double c8[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const double2 v = *(const double2 *)(sp + a0 + 2 * q);
+                c8[2 * q] = v.x;
+                c8[2 * q + 1] = v.y;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ix += (a0 + j < A && c8[j] < u) ? 1 : 0;
+        }
+        six[l] = ix;
+        wait_lds();
+        // lane a: the draws that chose action a
+        for (int k0 = 0; k0 < K; k0 += 4) {
+            const int4 v = *(const int4 *)(six + k0);
+            cnt += (v.x == l ? 1 : 0) + (k0 + 1 < K && v.y == l ? 1 : 0) + (k0 + 2 < K && v.z == l ? 1 : 0) +
+                   (k0 + 3 < K && v.w == l ? 1 : 0);
+        }
+        cursor += 2 * K;
+    }
+    if (MZ_STAMPS) {
+        asm volatile("" ::"v"(cnt));
+        stamp(tq, 2);
+    }
+    const long long st_old = (l < kStatN) ? sSt[l] : 0ll;
+    // the leaf's children (cnode.cpp:264-293), in ascending action order
+    wait_vm();  // the window landed: later waits need not drain this wave's stores
+    const int leaf = h.leaf;
+    int ncl = 0;
+    {
+        const bool hasc = (l < A) && cnt > 0;
+        const unsigned long long m = ballot(hasc);
+        ncl = __popcll(m);
+        int wild = 0;
+        if (tot + ncl > P) {
+            err |= kErrPool;
+            ncl = 0;
+        } else if (hasc) {
+            const int c = tot + __popcll(m & ((1ull << l) - 1ull));
+            const float bh = (float)cnt / (float)K;  // betahat_prob = count / sampled_times
+            const float prior = pol * bh / bet;      // prior * betahat_prob / beta_prob (no noise below the root)
+            if (!tame_prior(prior)) wild = 1;
+            const int4 a4 = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+            const int4 b4 = make_int4(0, pack_y(0, l, -1), f2i(0.0f), -1);
+            const size_t gi = nb + c;
+            d.A()[gi] = a4;
+            d.Bn()[gi] = b4;
+            d.C()[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+            d.D()[gi] = make_float4(pol, bet, bh, 0.f);
+            d.Q()[gi] = 0.f;
+            d.PP()[gi] = v_in;
+            d.Par()[gi] = leaf;
+            sA[c] = a4;
+            sB[c] = b4;
+            sPP[c] = v_in;
+            sFl[c] = 0;
+            sPS[c] = t00 * prior;  // prior score under the leaf after its first visit: pb_c(0, 0) * prior
+        }
+        if (ballot(wild != 0) || !tame_val(v_in) || !tame_val(r_in)) h.tame = 0;
+        if (!err && l == 0) {  // the leaf's structure: first child, children count, pred_value, hidden_state_index_x
+            const int ly = sB[leaf].y;
+            const int md = md_of(ly) < 0 ? 0 : md_of(ly);
+            const int4 nbv = make_int4(tot, pack_y(ncl, act_of(ly), md), f2i(v_in), hsx);
+            sB[leaf] = nbv;
+            d.Bn()[nb + leaf] = nbv;
+        }
+    }
+    if (l == 0) {
+        xi[15] = ncl;
+        xi[14] = err;
+    }
+    stamp(ts, 3);
+    lds_barrier();  // (2) back-propagation, prior scores, min/max partials and the children are in LDS
+    stamp(ts, 4);
+
+    // ---- the selection of the next simulation (cnode.cpp:381-413) ----
+    err |= uni(xi[8]);
+    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), unif(xf[4]));
+    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), unif(xf[5]));
+    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
+    const long long ent_r = xl[0], ent_w = xl[1];
+    const int ntot = err ? tot : tot + ncl;
+    unsigned long long tp[4] = {0};
+    int Dn = 0, x = 0, out_idx = 0, out_act = 0;
+    long long nscored = 0;
+    if constexpr (kTreeLevels<NC>) {
+        stamp(ts, 5);
+    if (!err) {
+        cursor = uni(cursor);
+        const bool mm_on = mm_cnt > 0;
+        float den = 0.f;
+        if (mm_on) {
+            const float delta = mmx - mmn;
+            den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
+        }
+        int px = 0, pvv = 0;
+        int xv = uni(sA[0].x) + 1;  // the root is on every path
+        int4 xb = uni4(sB[0]);
+        int par_hsx = xb.w;
+        pvv = wl(pvv, xv, 0);
+        while (true) {
+            x = uni(x);
+            xv = uni(xv);
+            cursor = uni(cursor);
+            const int nc = uni(nc_of(xb.y));
+            if (nc == 0) break;
+            const int fc = uni(xb.x);
+            // the children's records (lane j = child j), the next level's structure record included
+            const bool has = l < nc;
+            int4 ca = make_int4(0, 0, 0, 0), cb = ca;
+            float cpp = 0.f, cps = 0.f;
+            float2 caz = make_float2(0.f, 0.f);
+            int cfl = 0;
+            if (has) {
+                ca = sA[fc + l];
+                cb = sB[fc + l];
+                cpp = sPP[fc + l];
+                cps = sPS[fc + l];
+                cfl = sFl[fc + l];
+                caz = sAz[fc + l];
+            }
+            const int cvis = ca.x + (cfl ? 1 : 0);
+            int ci = 0;
+            if (x == 0 && xv <= nc) {
+                ci = xv - 1;  // forced root round-robin (cnode.cpp:398-399)
+            } else {
+                const int np = xv - 1;  // total_children_visit_counts = node->visit_count - 1
+                if (np < 0 || np >= PS) {
+                    err |= kErrTable;
+                    break;
+                }
+                nscored += nc;
+                float sc = -INFINITY;
+                if (has) {  // ucb_score (cnode.cpp:297-335)
+                    const float val = cfl ? caz.x : i2f(ca.z);
+                    const float rw = cfl ? caz.y : i2f(ca.w);
+                    float vs = (cvis == 0) ? 0.0f : ((rw + discount * val) - cpp);
+                    if (mm_on) vs = (vs - mmn) / den;
+                    if (vs < 0) vs = 0;
+                    if (vs > 1) vs = 1;
+                    sc = cps + vs;
+                }
+                float M;
+                if (nc <= 16) {  // one DPP row holds every child
+                    float v = sc;
+                    v = fmaxf(v, i2f(dpp<0xB1>(f2i(v))));
+                    v = fmaxf(v, i2f(dpp<0x4E>(f2i(v))));
+                    v = fmaxf(v, i2f(dpp<0x141>(f2i(v))));
+                    v = fmaxf(v, i2f(dpp<0x140>(f2i(v))));
+                    M = unif(v);
+                } else {
+                    M = unif(wave_max(sc));
+                }
+                // select_child's tie list (cnode.cpp:355-370) in closed form: the first maximum and
+                // every later child within epsilon of it; {s >= FLOAT_MIN} when no score beats FLOAT_MIN
+                unsigned long long lst;
+                if (M > -1000000.0f) {
+                    const unsigned long long first = ballot(has && sc == M);
+                    const int r = uni(__builtin_ctzll(first));
+                    lst = ballot(has && sc >= M - 0.000001f) & (~0ull << r);
+                } else {
+                    lst = ballot(has && sc >= -1000000.0f);
+                }
+                const int cntl = uni(__popcll(lst));
+                if (cntl > 0) {  // one engine word (gen() % size); its value matters only for ties
+                    if (cursor >= gW) {
+                        err |= kErrRng;
+                        break;
+                    }
+                    if (cntl > 1) {
+                        const int o = cursor - wbase;
+                        const unsigned w = (o >= 0 && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                                                                   : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                        for (int k = uni((int)(w % (unsigned)cntl)); k > 0; --k) lst &= lst - 1ull;
+                    }
+                    ++cursor;
+                    ci = uni(__builtin_ctzll(lst));
+                }
+            }
+            if (Dn + 1 >= PS) {
+                err |= kErrPath;
+                break;
+            }
+            par_hsx = uni(xb.w);
+            x = uni(fc + ci);
+            ++Dn;
+            xv = uni(rl(cvis, ci));
+            xb = make_int4(uni(rl(cb.x, ci)), uni(rl(cb.y, ci)), 0, uni(rl(cb.w, ci)));
+            if (Dn < kWave) {
+                px = wl(px, x, Dn);
+                pvv = wl(pvv, xv, Dn);
+            } else if (l == 0) {
+                sPath[Dn] = make_int2(x, xv);
+            }
+        }
+        if (Dn == 0) err |= kErrRoot;
+        wait_lds();
+        // the path {node, visits at selection} for the next back-propagation
+        int2 *gp = d.path() + (size_t)t * PS;
+        for (int i0 = 0; i0 <= Dn; i0 += kWave)
+            if (i0 + l <= Dn) gp[i0 + l] = (i0 == 0) ? make_int2(px, pvv) : sPath[i0 + l];
+        out_idx = (Dn == 0) ? uni(sB[0].w) : par_hsx;  // parent->hidden_state_index_x
+        out_act = act_of(uni(xb.y));                   // children_action of the last edge
+    }
+        stamp(tp, 3);
+    } else {
+        // every node's select_child outcome by the four waves (tree_select_prep), then the chase
+        tree_select_prep<NC>(smem, 0, ntot, discount, gdelta, PS, D, tp);
+        stamp(ts, 5);
+    if (!err) {
+        const int *nxt = (const int *)(smem + L::oPar);
+        const float2 *rec = (const float2 *)(smem + L::oAz);
+        cursor = uni(cursor);
+        int px = 0;
+        int v;
+        {
+            const int4 r0b = uni4(sB[0]);
+            const int rv = uni(sA[0].x) + 1;  // the root is on every path
+            const int nc0 = nc_of(r0b.y);
+            if (nc0 == 0) {
+                v = kTreeLeaf;
+            } else if (rv <= nc0) {
+                v = r0b.x + rv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
+            } else {
+                v = uni(nxt[0]);
+                if (v >= 0) ++cursor;
+            }
+        }
+        while (true) {
+            v = uni(v);
+            cursor = uni(cursor);
+            if (v < 0) {
+                if (v == kTreeLeaf) break;
+                // the exact record: ties (engine word modulo the list size), an empty list (child
+                // 0, no word) or a table error
+                const int xfl = uni(f2i(sQ[x]));
+                if (uni(xfl >> 16)) {
+                    err |= kErrTable;
+                    break;
+                }
+                const int cnt = uni(xfl & 0xffff);
+                int ci = 0;
+                if (cnt > 0) {
+                    const float2 rb = rec[x];
+                    unsigned long long lst = ((unsigned long long)(unsigned)uni(f2i(rb.y)) << 32) |
+                                             (unsigned)uni(f2i(rb.x));
+                    if (cursor >= gW) {
+                        err |= kErrRng;
+                        break;
+                    }
+                    if (cnt > 1) {
+                        const int o = cursor - wbase;
+                        const unsigned w = (o >= 0 && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                                                                   : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                        for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
+                    }
+                    ++cursor;
+                    ci = uni(__builtin_ctzll(lst));
+                }
+                v = uni(uni(sB[x].x) + ci);
+            }
+            if (Dn + 1 >= PS) {
+                err |= kErrPath;
+                break;
+            }
+            x = v;
+            ++Dn;
+            if (Dn < kWave) px = wl(px, x, Dn);
+            else if (l == 0) sPath[Dn] = make_int2(x, 0);
+            v = uni(nxt[x]);
+            if (v >= 0) ++cursor;
+        }
+        if (cursor > gW) err |= kErrRng;  // a consumed word beyond the stream
+        if (Dn == 0) err |= kErrRoot;
+        wait_lds();
+        // the path {node, visits at selection} for the next back-propagation, the scored children
+        // and the outputs, by the whole wave
+        int2 *gp = d.path() + (size_t)t * PS;
+        int nsc = 0, xpar = 0;
+        for (int i0 = 0; i0 <= Dn; i0 += kWave) {
+            const int i = i0 + l;
+            if (i <= Dn) {
+                const int xi_ = (i < kWave) ? px : sPath[i].x;
+                const int vis = sA[xi_].x + (sFl[xi_] ? 1 : 0);
+                gp[i] = make_int2(xi_, vis);
+                const int4 bi = sB[xi_];
+                if (i < Dn && !(i == 0 && vis <= nc_of(bi.y))) nsc += nc_of(bi.y);  // scored levels
+                if (i == Dn - 1) xpar = bi.w;
+            }
+        }
+        nscored = wave_sum(nsc);
+        out_idx = (Dn == 0) ? uni(sB[0].w) : uni(rl(xpar, (Dn - 1) & (kWave - 1)));  // parent->hidden_state_index_x
+        out_act = act_of(uni(sB[x].y));                                             // children_action of the last edge
+    }
+    }
+    stamp(ts, 6);
+    if (l == 0) {
+        idx_x[t] = err ? 0 : out_idx;
+        idy[t] = t;
+        act[t] = err ? 0 : out_act;
+    }
+    // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[idx_x][t]
+    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+    bool gath_reg = false, gath_lds = false;
+    char *gdst = nullptr;
+    unsigned char *sbig = smem + L::oReg;  // (wave 1's value entries are done)
+    if (pool && !err) {
+        const char *src = pool + (long long)out_idx * pool_stride + (long long)t * row_bytes;
+        gdst = gather_out + (long long)t * row_bytes;
+        const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) &
+                         15) == 0;
+        const long long o = (long long)l * 16;
+        if (al && row_bytes <= 4 * 16 * kWave) {
+            if (o < row_bytes) gv0 = *(const int4 *)(src + o);
+            if (o + 1024 < row_bytes) gv1 = *(const int4 *)(src + o + 1024);
+            if (o + 2048 < row_bytes) gv2 = *(const int4 *)(src + o + 2048);
+            if (o + 3072 < row_bytes) gv3 = *(const int4 *)(src + o + 3072);
+            gath_reg = true;
+        } else if (al && row_bytes <= 16 * 16 * kWave && row_bytes <= 8ll * kRegCap) {
+            const long long last = row_bytes - 16;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+            gath_lds = true;
+        } else if (al) {
+            for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(gdst + o2) = *(const int4 *)(src + o2);
+        } else {
+            for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
+                *(int *)(gdst + o2) = *(const int *)(src + o2);
+        }
+    }
+    stamp(ts, 7);
+    {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
+        const int cur = err ? h.cursor : cursor;
+        const int o = cur + l - wbase;
+        TreeHdr *hp = d.hdr() + t;
+        if (l < kNxt)
+            hp->nxt[l] = (o >= 0 && o < kRngWin) ? sRng[o] : ((cur + l < gW) ? d.R()[(size_t)t * gW + cur + l] : 0u);
+        if (l == 0) {
+            hp->cursor = cur;
+            hp->tot = err ? h.tot : ntot;
+            hp->D = err ? h.D : Dn;
+            hp->err = err;
+            hp->mm_min = mmn;
+            hp->mm_max = mmx;
+            hp->mm_cnt = mm_cnt;
+            hp->tame = h.tame;
+            hp->leaf = err ? h.leaf : x;
+        }
+    }
+    if (gath_lds) {
+        wait_vm();
+        for (long long o = (long long)l * 16; o < row_bytes; o += 16 * kWave) *(int4 *)(gdst + o) = *(const int4 *)(sbig + o);
+    }
+    if (gath_reg) {
+        const long long o = (long long)l * 16;
+        if (o < row_bytes) *(int4 *)(gdst + o) = gv0;
+        if (o + 1024 < row_bytes) *(int4 *)(gdst + o + 1024) = gv1;
+        if (o + 2048 < row_bytes) *(int4 *)(gdst + o + 2048) = gv2;
+        if (o + 3072 < row_bytes) *(int4 *)(gdst + o + 3072) = gv3;
+    }
+    stamp(ts, 8);
+    if (l < kStatN) {
+        long long add = 0;
+        switch (l) {
+            case MZ_S_SELECTS: add = err ? 0 : 1; break;
+            case MZ_S_PATH_EDGES: add = Dn; break;
+            case MZ_S_SCORED: add = nscored; break;
+            case MZ_S_EXPANDS: add = 1; break;
+            case MZ_S_NEW_CHILDREN: add = ncl; break;
+            case MZ_S_BACKUP_NODES: add = D + 1; break;
+            case MZ_S_ENTRIES_READ: add = ent_r; break;
+            case MZ_S_ENTRIES_WRITTEN: add = ent_w; break;
+            case MZ_S_MINMAX_NODES: add = tot - 1; break;
+            case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;    // round 1
+            case MZ_S_CYC_STAGE2: add = (long long)(ts[2] - ts[1]); break;    // barrier (1) wait
+            case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;    // draws + children
+            case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;    // barrier (2) wait
+            case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;    // scores + tie lists (4 waves)
+            case MZ_S_CYC_STAGE1: add = (long long)(tp[0] - ts[4]); break;    // (scores)
+            case MZ_S_CYC_W1_SYNC: add = (long long)(tp[1] - tp[0]); break;   // (barrier + tie lists)
+            case MZ_S_CYC_SELECT: add = (long long)(tp[3] - ts[5]); break;    // the chase
+            case MZ_S_CYC_BAK_WAIT: add = (long long)(ts[6] - tp[3]); break;  // path record + outputs
+            case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;
+            case MZ_S_CYC_EPILOGUE: add = (long long)(ts[8] - ts[7]); break;
+            case MZ_S_STAMPED: add = 1; break;
+            case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1 after barrier (1)
+            case MZ_S_CYC_EXP_CDF: add = (long long)(tq[0] - ts[0]); break;   // round 1 landed
+            case MZ_S_CYC_EXP_DRAW: add = (long long)(tq[1] - tq[0]); break;  // sampling distribution
+            case MZ_S_CYC_EXP_NODES: add = (long long)(tq[2] - tq[1]); break; // K draws
+            case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? xl[3] : 0; break;       // wave 1: staging issue
+            case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? xl[5] : 0; break;      // wave 1: entries landed
+            case MZ_S_CYC_W1_ROUND1: add = MZ_STAMPS ? xl[6] : 0; break;      // wave 1: node updates
+            default: break;
+        }
+        st[l] = st_old + add;
+    }
+    if (l == 0 && err) atomicOr(d.err(), err);
+}
+
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
 // One device word, set by a kernel.  Captured search graphs never hold a runtime memset node: under
 // the HIP runtime's graph packet capture, a replayed hipMemsetAsync node can write a stale fill
@@ -2796,6 +3872,7 @@ struct mz_batch {
     long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
     int nc = 0;                // k_step layout class (0 = layout from Geo)
     int chain_nc = -1;         // k_chain node class for K = 1 trees (-1: k_step for every launch)
+    int tree_nc = -1;          // k_tree node class for 2 <= K <= 64 trees (-1: k_step)
     Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
 };
 
@@ -2955,6 +4032,15 @@ void launch_chain(mz_batch *b, const StepArgs &a, int lds) {
                        a.act);
 }
 
+template <int NC>
+void launch_tree(mz_batch *b, const StepArgs &a) {
+    const Geo &g = b->geo;
+    hipLaunchKernelGGL((k_tree<NC>), dim3(g.B), dim3(4 * kWave), TreeLayout<NC>::total, b->stream,
+                       (char *)b->dev.base, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value,
+                       a.policy, a.beta, a.K, a.hsx, a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes,
+                       a.gather_out, a.idx_x, a.idy, a.act);
+}
+
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
     if (eb && sel && b->chain_nc >= 0) {  // K = 1 trees: the chain kernel
@@ -2980,6 +4066,20 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         a.ne = (int)(ne < g.P ? ne : g.P);
         const long long pe = b->expansions + 1;
         a.pe = (int)(pe < g.PS ? pe : g.PS);
+    }
+    if (eb && sel && b->tree_nc > 0) {  // 2 <= K <= 64 trees: the four-wave kernel
+        switch (b->tree_nc) {
+            case 64: launch_tree<64>(b, a); break;
+            case 128: launch_tree<128>(b, a); break;
+            case 256: launch_tree<256>(b, a); break;
+            case 384: launch_tree<384>(b, a); break;
+            case 512: launch_tree<512>(b, a); break;
+            default: launch_tree<1024>(b, a); break;
+        }
+        HIP_TRY(hipGetLastError());
+        b->rb_valid = b->rb_dev_valid = false;
+        ++b->expansions;
+        return MZ_OK;
     }
 #ifndef MZ_NO_JOINT
     if (b->N > 1) {
@@ -3194,6 +4294,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             }
         if (chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave > 160 * 1024) b->chain_nc = -1;
     }
+    if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && !getenv_flag("MZ_NO_TREE")) b->tree_nc = b->nc;
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
@@ -3270,6 +4371,18 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             case 512: set_lds_limit<512>(g.lds); break;
             case 1024: set_lds_limit<1024>(g.lds); break;
             default: set_lds_limit<0>(g.lds); break;
+        }
+    }
+    if (b->tree_nc > 0 && tree_lds_bytes(b->tree_nc) > 64 * 1024) {
+        const auto attr = hipFuncAttributeMaxDynamicSharedMemorySize;
+        const int tl = tree_lds_bytes(b->tree_nc);
+        switch (b->tree_nc) {
+            case 64: (void)hipFuncSetAttribute((const void *)k_tree<64>, attr, tl); break;
+            case 128: (void)hipFuncSetAttribute((const void *)k_tree<128>, attr, tl); break;
+            case 256: (void)hipFuncSetAttribute((const void *)k_tree<256>, attr, tl); break;
+            case 384: (void)hipFuncSetAttribute((const void *)k_tree<384>, attr, tl); break;
+            case 512: (void)hipFuncSetAttribute((const void *)k_tree<512>, attr, tl); break;
+            default: (void)hipFuncSetAttribute((const void *)k_tree<1024>, attr, tl); break;
         }
     }
     if (b->chain_nc >= 0) {

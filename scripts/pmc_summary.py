@@ -49,7 +49,7 @@ def main():
         short = k.replace("void ", "").replace("(anonymous namespace)::", "")
         short = re.sub(r"\(.*$", "", short).replace(" ", "")
         kernels[short] = dict(fetch_kb=fetch.get(k), write_kb=write.get(k), dispatches=max(nf.get(k, 0), nw.get(k, 0)))
-    fused = next((v for k, v in kernels.items() if k.startswith("k_step<true,true")), {})
+    fused = next((v for k, v in kernels.items() if k.startswith("k_chain<") or k.startswith("k_step<true,true")), {})
     out = {}
     if os.path.exists(args.out):
         out = json.load(open(args.out))
