@@ -145,17 +145,15 @@ class HipLeg:
         S, K, c2, c1, g = self.S, self.K, self.c2, self.c1, self.g
         tb = sd["tb"]
         out = (sd["idx"], sd["idy"], sd["act"])
-        tb.prepare(sd["rr"], sd["rv"], sd["rp"], sd["rb"], K, sd["eps"], sd["rn"])
-        tb.batch_selection_device(c2, c1, g, out=out)
+        tb.prepare_selection_device(sd["rr"], sd["rv"], sd["rp"], sd["rb"], K, sd["eps"], sd["rn"], c2, c1, g, out=out)
         for s in range(S):
             if s + 1 < S:
                 tb.expansion_backup_selection_device(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s],
                                                      c2, c1, out=out, pool=sd["pool"], gather_out=sd["leaf"])
             else:
                 tb.batch_expansion_and_backup(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s])
-        # search outputs stay on the device (mcts_sampled.py:176-191)
-        self.lib.mz_get_roots_values(tb._h, C.c_void_p(sd["values"].data_ptr()), 1)
-        self.lib.mz_get_roots_marginal_visit_count(tb._h, C.c_void_p(sd["visits"].data_ptr()), 1)
+        # search outputs stay on the device (mcts_sampled.py:176-191): one readback launch
+        tb.get_roots_device(g, values=sd["values"], marginal_visit_count=sd["visits"])
 
     def env_step(self):
         for sd in self.searches:  # agents searched sequentially (selfplay_worker.py:196-211)

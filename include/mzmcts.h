@@ -156,6 +156,15 @@ int mz_expand_backup_select(mz_batch *b, int hidden_state_index_x, float discoun
                             const void *pool, int64_t pool_slot_stride, int64_t row_bytes,
                             void *gather_out);
 
+/* Fused device path (no reference counterpart): mz_prepare followed by mz_select in one launch.
+ * Right after prepare the root has one visit and at least one child, so the first selection is
+ * the forced round-robin child 0 (cnode.cpp:398-399, no scoring, no engine word): identical
+ * results to the two calls.  Device memory only. */
+int mz_prepare_select(mz_batch *b, const float *rewards, const float *values, const float *policy_probs,
+                      const float *beta, int sampled_times, float noise_eps, const float *noises,
+                      float pb_c_base, float pb_c_init, float discount,
+                      int32_t *idx_x, int32_t *idy, int32_t *actions);
+
 /* Standalone hidden-state gather (mcts_sampled.py:130-134): out[i] = pool[idx_x[i]][i].
  * Device memory only; row_bytes must be a multiple of 4. */
 int mz_gather_rows(mz_batch *b, const void *pool, int64_t pool_slot_stride, int64_t row_bytes,
@@ -178,6 +187,20 @@ int mz_max_children(mz_batch *b, int32_t *out);
  * with zeros past each root's degree; degrees [B] (may be NULL). */
 int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *out,
                                 int32_t *degrees, int mem);
+
+/* Every readback above for all roots in one launch, written straight into device buffers
+ * (mcts_sampled.py:176-191 reads them all after each search); a NULL entry is not written.
+ * values [B]; marginal_* [B, agent_num, A]; degrees [B]; sampled[f] is the MZ_F_* field f as
+ * mz_get_roots_sampled_padded lays it out ([B, max_children(, agent_num)], zero-padded).
+ * Device memory only; stream-ordered, no synchronisation. */
+typedef struct {
+    float *values;
+    int32_t *marginal_visit_count;
+    float *marginal_priors;
+    int32_t *degrees;
+    void *sampled[MZ_F_COUNT];
+} mz_readback_out;
+int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out);
 
 /* --- diagnostics ----------------------------------------------------------------------- */
 /* Counters accumulated since creation (MZ_S_COUNT int64 values); host memory. */

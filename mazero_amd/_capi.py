@@ -29,6 +29,17 @@ FIELDS = {
 }
 INT_FIELDS = {"actions", "visit_count"}
 
+
+class ReadbackOut(C.Structure):
+    """mz_readback_out (include/mzmcts.h): device destinations of mz_get_roots_device."""
+    _fields_ = [
+        ("values", C.c_void_p),
+        ("marginal_visit_count", C.c_void_p),
+        ("marginal_priors", C.c_void_p),
+        ("degrees", C.c_void_p),
+        ("sampled", C.c_void_p * len(FIELDS)),
+    ]
+
 STATS = [
     "selects",
     "path_edges",
@@ -73,6 +84,7 @@ EXPORTS = [
     "mz_select",
     "mz_expand_backup",
     "mz_expand_backup_select",
+    "mz_prepare_select",
     "mz_gather_rows",
     "mz_get_roots_values",
     "mz_get_roots_marginal_visit_count",
@@ -81,6 +93,7 @@ EXPORTS = [
     "mz_get_root_sampled",
     "mz_max_children",
     "mz_get_roots_sampled_padded",
+    "mz_get_roots_device",
     "mz_get_stats",
     "mz_print",
 ]
@@ -126,6 +139,7 @@ def bind(lib: C.CDLL) -> C.CDLL:
             _i,
             [_p, _i, _f, _i, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _i64, _i64, _p],
         ),
+        "mz_prepare_select": (_i, [_p, _p, _p, _p, _p, _i, _f, _p, _f, _f, _f, _p, _p, _p]),
         "mz_gather_rows": (_i, [_p, _p, _i64, _i64, _p, _p]),
         "mz_get_roots_values": (_i, [_p, _p, _i]),
         "mz_get_roots_marginal_visit_count": (_i, [_p, _p, _i]),
@@ -134,6 +148,7 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "mz_get_root_sampled": (_i, [_p, _i, _i, _f, _p]),
         "mz_max_children": (_i, [_p, _p]),
         "mz_get_roots_sampled_padded": (_i, [_p, _i, _f, _p, _p, _i]),
+        "mz_get_roots_device": (_i, [_p, _f, _p]),
         "mz_get_stats": (_i, [_p, _p]),
         "mz_print": (_i, [_p]),
     }

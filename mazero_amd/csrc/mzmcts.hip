@@ -145,6 +145,7 @@ struct PrepArgs {
     const float *reward, *value, *policy, *beta, *noise;
     float eps;
     int K;
+    int *idx_x, *idy, *act;  // non-null: also the first selection (mz_prepare_select)
 };
 
 // Per-handle constants, written once to device memory at mz_create: kernels take a pointer to
@@ -560,7 +561,8 @@ __device__ __forceinline__ double cdf_lane(double bd, int A) {
 // --------------------------------------------------------------------------------------------
 __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float pol, float bet, float noi, float eps,
                            int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
-                           long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl, int &wild) {
+                           long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl, int &wild,
+                           int *first_act = nullptr) {
     const int l = lane_id();
     const int A = g.A;
     int cnt = 0;  // number of draws that hit action l
@@ -606,6 +608,7 @@ __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, in
     const bool has = (l < A) && cnt > 0;
     const unsigned long long m = ballot(has);
     const int nc = __popcll(m);
+    if (first_act) *first_act = m ? (int)__builtin_ctzll(m) : 0;  // the first child's action (ascending order)
     if (tot + nc > g.P) {
         err |= kErrPool;
         return 0;
@@ -783,6 +786,10 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     __shared__ unsigned w0[kMtN];
     const int t = blockIdx.x;
     const int tid = threadIdx.x;
+    // the handle's error word starts clean (no runtime memset node in captured graphs).  A tree's
+    // error also stays in its header, and every later kernel re-reports the errors of dead trees,
+    // so an error raised by another block before this store is not lost.
+    if (t == 0 && tid == 0) *d.err() = 0;
     if (tid == 0) {  // std::mt19937::seed: sequential by definition
         unsigned x = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
         mt[0] = x;
@@ -835,6 +842,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     int cursor = 0, tot = 1;
     long long st_new = 0;
     int nc;
+    int first_act = 0;
     int wild = (g.N > 1) ? 1 : 0;  // joint-action trees always take the exact selection
     if (g.N > 1) {  // joint actions: the root's [N][A] inputs staged in (dynamic) LDS
         extern __shared__ __attribute__((aligned(16))) unsigned char jsm[];
@@ -857,7 +865,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         const float bet = (l < A) ? a.beta[ib + l] : 0.f;
         const float noi = (l < A) ? a.noise[ib + l] : 0.f;
         nc = expand_node(g, d, t, 0, pol, bet, noi, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, err, st_new, false, 0u,
-                         0u, nullptr, wild);
+                         0u, nullptr, wild, &first_act);
     }
     if (l == 0) {
         // root: CNode(1,1,1,1,true) (cnode.cpp:217), expanded, visit += 1, subtree.update(value, 0)
@@ -876,22 +884,46 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         d.Q()[gi] = 0.f;
         d.PP()[gi] = 0.f;
         d.V()[gi * g.E] = make_int2(0, f2i(v));
+        // mz_prepare_select: the first selection (select_path, cnode.cpp:381-413) right after
+        // prepare: the root has one visit and nc >= 1 children, so the forced round-robin takes
+        // child 0 (cnode.cpp:398-399) without scoring and without an engine word
+        const bool sel = a.idx_x != nullptr;
+        int D = 0, leaf = 0, sact = 0;
+        if (sel && !err) {
+            if (nc > 0) {
+                D = 1;
+                leaf = 1;  // the root's first child
+                sact = first_act;
+            } else {
+                err |= kErrRoot;
+            }
+        }
         TreeHdr h;
         h.cursor = cursor;
         h.tot = tot;
-        h.D = 0;
+        h.D = D;
         h.err = err;
         h.mm_min = 0.f;
         h.mm_max = 0.f;
         h.mm_cnt = 0;
-        h.leaf = 0;
+        h.leaf = leaf;
         h.tame = (!wild && tame_val(v) && tame_val(r)) ? 1 : 0;
         for (int j = 0; j < kNxt; ++j) h.nxt[j] = (cursor + j < kMtN) ? w0[cursor + j] : 0u;
         d.hdr()[t] = h;
         d.path()[(size_t)t * g.PS] = make_int2(0, 1);
+        if (D == 1) d.path()[(size_t)t * g.PS + 1] = make_int2(1, 0);
         long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
         st[MZ_S_EXPANDS] += 1;
         st[MZ_S_NEW_CHILDREN] += st_new;
+        if (sel) {
+            a.idx_x[t] = 0;  // the root's hidden_state_index_x
+            a.idy[t] = t;
+            a.act[t] = err ? 0 : sact;
+            if (!err) {
+                st[MZ_S_SELECTS] += 1;
+                st[MZ_S_PATH_EDGES] += 1;
+            }
+        }
         if (err) atomicOr(d.err(), err);
     }
 }
@@ -1950,7 +1982,8 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
         return;
     }
 #endif
-    if (h.err) {  // a dead tree stays dead (both waves see the same header)
+    if (h.err) {  // a dead tree stays dead (both waves see the same header) and re-reports its error
+        if (wv == 0 && l == 0) atomicOr(d.err(), h.err);
         if (SEL && wv == 0) {
             if (l == 0) {
                 a.idx_x[t] = 0;
@@ -2398,7 +2431,7 @@ __device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp)
     return cp;
 }
 
-template <int NC>
+template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
 __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA, int pk, const float *reward,
                                                const float *value, const float *policy, const float *beta, int K,
                                                int hsx, float discount, int fast_ok, const char *pool,
@@ -2432,8 +2465,8 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     int4 leaf_b = make_int4(0, 0, 0, 0);
     // the next leaf's parent is this launch's leaf (hidden_state_index_x = hsx): its row is
     // fetched now and stored at the end (four 16-byte chunks per lane up to 4 KiB, LDS-DMA above)
-    const bool row_al = pool && (((row_bytes | pool_stride | (long long)(uintptr_t)pool |
-                                   (long long)(uintptr_t)gather_out) & 15) == 0);
+    const bool row_al = SEL && pool && (((row_bytes | pool_stride | (long long)(uintptr_t)pool |
+                                          (long long)(uintptr_t)gather_out) & 15) == 0);
     const bool g_reg = row_al && row_bytes <= 4 * 16 * kWave;
     const bool g_lds = row_al && !g_reg && row_bytes <= 16 * 16 * kWave;
     int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
@@ -2489,12 +2522,15 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     const unsigned oR = pl->d.o_R;
     d.o_D = pl->d.o_D;
     wait_vm();
-    if (h.err) {  // a dead tree stays dead (both waves see the same header)
+    if (h.err) {  // a dead tree stays dead (both waves see the same header) and re-reports its error
         if (wv == 0) {
             if (l == 0) {
-                idx_x[t] = 0;
-                idy[t] = t;
-                act[t] = 0;
+                if (SEL) {
+                    idx_x[t] = 0;
+                    idy[t] = t;
+                    act[t] = 0;
+                }
+                atomicOr(d.err(), h.err);
             }
         }
         return;
@@ -2504,9 +2540,11 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     if (D != Dp || h.tot != D + 1 || h.leaf != D) {
         if (D + 1 > P || h.tot != D + 1 || h.leaf != D) {  // not a chain: refuse (reported below)
             if (wv == 0 && l == 0) {
-                idx_x[t] = 0;
-                idy[t] = t;
-                act[t] = 0;
+                if (SEL) {
+                    idx_x[t] = 0;
+                    idy[t] = t;
+                    act[t] = 0;
+                }
                 TreeHdr *hp = d.hdr() + t;
                 hp->err = kErrPath;
                 atomicOr(d.err(), kErrPath);
@@ -2582,17 +2620,17 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
         d.Bn()[nb + leaf] = make_int4(c, pack_y(1, act_of(leaf_b.y), md), f2i(v_in), hsx);
     }
     const int tame = (h.tame && !wild && tame_val(v_in) && tame_val(r_in)) ? 1 : 0;
-    const bool fast = fast_ok && tame && fabsf(discount) <= 1.0f;
+    const bool fast = !SEL || (fast_ok && tame && fabsf(discount) <= 1.0f);  // (no selection: no words)
     // the selection on a tame tree (select_walk): the new child; one word per level but the
     // forced first one (root visits after this back-propagation = the staged count + 1)
     const int Ds = c;
     int root_visit = 0, words = 0;
-    if (fast) {
+    if (SEL && fast) {
         root_visit = uni(sA[0].x) + 1;
         if (root_visit - 1 >= PS) err |= kErrTable;
         words = Ds - ((root_visit <= 1) ? 1 : 0);
     }
-    if (Ds + 1 > PS) err |= kErrPath;
+    if (SEL && Ds + 1 > PS) err |= kErrPath;
     // the next expansion's engine words, for the header (in flight during the back-propagation)
     unsigned nxt_w = 0;
     const unsigned *Rt = (const unsigned *)(base + (size_t)oR * 256) + (size_t)t * gW;
@@ -2631,7 +2669,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     mx = unif(rlf(wave_max_to63(mx), 63));
     const int mm_cnt = D;
 
-    if (!fast && !err) {
+    if (SEL && !fast && !err) {
         // ---- select_walk's exact case: every level's tie list must be non-empty to consume a
         // word (score >= FLOAT_MIN, not NaN); levels 1..Ds scored in parallel ----
         sA[c] = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
@@ -2673,12 +2711,12 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     }
 
     // ---- outputs (mcts_sampled.py:123-134), the header, the statistics ----
-    if (l == 0) {
+    if (SEL && l == 0) {
         idx_x[t] = err ? 0 : hsx;  // parent->hidden_state_index_x: the expanded leaf's
         idy[t] = t;
         act[t] = err ? 0 : a;
     }
-    if (pool && !err) {
+    if (SEL && pool && !err) {
         const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
         char *dst = gather_out + (long long)t * row_bytes;
         const long long o = (long long)l * 16;
@@ -2702,21 +2740,21 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
         if (l == 0) {
             hp->cursor = err ? h.cursor : cursor + words;
             hp->tot = err ? h.tot : c + 1;
-            hp->D = err ? h.D : Ds;
+            hp->D = (err || !SEL) ? h.D : Ds;
             hp->err = err;
             hp->mm_min = mn;
             hp->mm_max = mx;
             hp->mm_cnt = mm_cnt;
             hp->tame = tame;
-            hp->leaf = err ? h.leaf : c;
+            hp->leaf = (err || !SEL) ? h.leaf : c;
         }
     }
     if (l < MZ_S_CYC_HEADER) {
         long long add = 0;
         switch (l) {
-            case MZ_S_SELECTS: add = 1; break;
-            case MZ_S_PATH_EDGES: add = Ds; break;
-            case MZ_S_SCORED: add = Ds; break;
+            case MZ_S_SELECTS: add = SEL ? 1 : 0; break;
+            case MZ_S_PATH_EDGES: add = SEL ? Ds : 0; break;
+            case MZ_S_SCORED: add = SEL ? Ds : 0; break;
             case MZ_S_EXPANDS: add = 1; break;
             case MZ_S_NEW_CHILDREN: add = 1; break;
             case MZ_S_BACKUP_NODES: add = D + 1; break;
@@ -3041,7 +3079,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
     lds_barrier();  // (4)
 }
 
-template <int NC>
+template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
 __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA, int pk, const float *reward,
                                               const float *value, const float *policy, const float *beta, int K,
                                               int hsx, float discount, int fast_ok, const char *pool,
@@ -3132,7 +3170,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 const int np = sA[p].x + (sFl[p] ? 1 : 0) - 1;  // the parent's total child visits, after
                 const int fn = sFl[n];
                 int v = a.x + (fn ? 1 : 0);
-                if (np >= 0 && np < PS) {
+                if (SEL && np >= 0 && np < PS) {
                     if (v > np) v = np;  // (not in a consistent tree; keeps the read in range)
                     pbc[k] = T[np * (np + 1) / 2 + v];
                 }
@@ -3144,10 +3182,12 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 }
             }
         }
+        if constexpr (SEL) {
 #pragma unroll
-        for (int k = 0; k < NBW; ++k) {
-            const int n = (2 * k + wv - 2) * kWave + l;
-            if (n >= 1 && n < tot) sPS[n] = pbc[k] * i2f(sA[n].y);  // pb_c * prior (cnode.cpp:316)
+            for (int k = 0; k < NBW; ++k) {
+                const int n = (2 * k + wv - 2) * kWave + l;
+                if (n >= 1 && n < tot) sPS[n] = pbc[k] * i2f(sA[n].y);  // pb_c * prior (cnode.cpp:316)
+            }
         }
         cv = wave_sum(cv);
         mn = wave_min_to63(mn);
@@ -3158,7 +3198,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         }
         if (l == 0) xi[7 + wv] = cv;
         lds_barrier();  // (2)
-        if constexpr (!kTreeLevels<NC>) {
+        if constexpr (SEL && !kTreeLevels<NC>) {
             const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[14]);
             tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, pl->g.delta, PS, hp0->D);
         }
@@ -3244,7 +3284,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
             }
         }
         lds_barrier();  // (2): its global stores stay in flight
-        if constexpr (!kTreeLevels<NC>) {
+        if constexpr (SEL && !kTreeLevels<NC>) {
             const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[14]);
             tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, pl->g.delta, PS, D);
         }
@@ -3294,11 +3334,14 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // round 1 landed (the window may not have)
     unsigned long long tq[4] = {0};
     stamp(tq, 0);
-    if (h.err) {  // a dead tree stays dead (every wave reads the same header)
+    if (h.err) {  // a dead tree stays dead (every wave reads the same header) and re-reports its error
         if (l == 0) {
-            idx_x[t] = 0;
-            idy[t] = t;
-            act[t] = 0;
+            if (SEL) {
+                idx_x[t] = 0;
+                idy[t] = t;
+                act[t] = 0;
+            }
+            atomicOr(d.err(), h.err);
         }
         wait_vm();
         return;
@@ -3428,7 +3471,9 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     unsigned long long tp[4] = {0};
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
     long long nscored = 0;
-    if constexpr (kTreeLevels<NC>) {
+    if constexpr (!SEL) {
+        stamp(ts, 5);
+    } else if constexpr (kTreeLevels<NC>) {
         stamp(ts, 5);
     if (!err) {
         cursor = uni(cursor);
@@ -3639,7 +3684,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     }
     }
     stamp(ts, 6);
-    if (l == 0) {
+    if (SEL && l == 0) {
         idx_x[t] = err ? 0 : out_idx;
         idy[t] = t;
         act[t] = err ? 0 : out_act;
@@ -3649,7 +3694,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     bool gath_reg = false, gath_lds = false;
     char *gdst = nullptr;
     unsigned char *sbig = smem + L::oReg;  // (wave 1's value entries are done)
-    if (pool && !err) {
+    if (SEL && pool && !err) {
         const char *src = pool + (long long)out_idx * pool_stride + (long long)t * row_bytes;
         gdst = gather_out + (long long)t * row_bytes;
         const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) &
@@ -3683,13 +3728,13 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         if (l == 0) {
             hp->cursor = cur;
             hp->tot = err ? h.tot : ntot;
-            hp->D = err ? h.D : Dn;
+            hp->D = (err || !SEL) ? h.D : Dn;
             hp->err = err;
             hp->mm_min = mmn;
             hp->mm_max = mmx;
             hp->mm_cnt = mm_cnt;
             hp->tame = h.tame;
-            hp->leaf = err ? h.leaf : x;
+            hp->leaf = (err || !SEL) ? h.leaf : x;
         }
     }
     if (gath_lds) {
@@ -3707,7 +3752,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     if (l < kStatN) {
         long long add = 0;
         switch (l) {
-            case MZ_S_SELECTS: add = err ? 0 : 1; break;
+            case MZ_S_SELECTS: add = (err || !SEL) ? 0 : 1; break;
             case MZ_S_PATH_EDGES: add = Dn; break;
             case MZ_S_SCORED: add = nscored; break;
             case MZ_S_EXPANDS: add = 1; break;
@@ -3774,23 +3819,36 @@ __global__ __launch_bounds__(64) void k_gather(const char *pool, long long strid
 //   [B] root value | [B*A] marginal visits | [B*A] marginal priors | [B] degree |
 //   MZ_F_COUNT x [B*Wd] per-child fields padded with zeros to Wd = max degree
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm, float disc, int Wd, int *out) {
+// Destinations of one k_readback launch: the handle's packed buffer (readback_dev) or the caller's
+// device buffers (mz_get_roots_device); a null field is not written.  Per-child fields are
+// [B][Wd(*N)] either way.
+struct RbPtrs {
+    float *values;  // [B]
+    int *mv;        // [B][N*A] marginal visit counts
+    float *mp;      // [B][N*A] marginal priors
+    int *deg;       // [B] root degrees
+    int *f[MZ_F_COUNT];
+};
+
+__global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm, float disc, int Wd, RbPtrs o) {
     const Geo g = prm->g;
     const Dev d = prm->d;
     const int t = blockIdx.x;
     const int l = threadIdx.x;
-    const int B = g.B, A = g.A;
-    (void)A;
+    const int A = g.A;
     const size_t nb = (size_t)t * g.P;
     const int4 ra = d.A()[nb];
     const int4 rbn = d.Bn()[nb];
     const int nc = nc_of(uni(rbn.y));
     const int fc = uni(rbn.x);
-    float *fout = (float *)out;
+    {
+        const int herr = d.hdr()[t].err;  // dead trees re-report their error (see k_prepare)
+        if (l == 0 && herr) atomicOr(d.err(), herr);
+    }
     const int N = g.N, NA = g.NA;
     if (l == 0) {
-        fout[t] = (nc > 0) ? i2f(ra.z) : 0.f;
-        out[B + 2 * B * NA + t] = nc;
+        if (o.values) o.values[t] = (nc > 0) ? i2f(ra.z) : 0.f;
+        if (o.deg) o.deg[t] = nc;
     }
     const bool has = l < nc;
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
@@ -3804,42 +3862,39 @@ __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm,
     const unsigned char *jt = d.J() + (size_t)t * g.JP + (size_t)fc * N;  // joint actions (N > 1)
     // marginal visit counts / priors (cnode.cpp:69-91): cell (agent j, action a) collects, in child
     // order, every child whose action for agent j is a
-    for (int cell = l; cell < NA; cell += kWave) {
-        const int j = cell / A, av = cell - j * A;
-        int mv = 0;
-        float mp = 0.f;
-        for (int c = 0; c < nc; ++c) {
-            const int aj = (N == 1) ? rl(act, c) : (int)jt[c * N + j];
-            const int vj = rl(ca.x, c);
-            const float pj = rlf(i2f(ca.y), c);
-            if (aj == av) {
-                mv += vj;
-                mp += pj;
+    if (o.mv || o.mp)
+        for (int cell = l; cell < NA; cell += kWave) {
+            const int j = cell / A, av = cell - j * A;
+            int mv = 0;
+            float mp = 0.f;
+            for (int c = 0; c < nc; ++c) {
+                const int aj = (N == 1) ? rl(act, c) : (int)jt[c * N + j];
+                const int vj = rl(ca.x, c);
+                const float pj = rlf(i2f(ca.y), c);
+                if (aj == av) {
+                    mv += vj;
+                    mp += pj;
+                }
             }
+            if (o.mv) o.mv[(size_t)t * NA + cell] = mv;
+            if (o.mp) o.mp[(size_t)t * NA + cell] = mp;
         }
-        out[B + (size_t)t * NA + cell] = mv;
-        fout[B + (size_t)B * NA + (size_t)t * NA + cell] = mp;
-    }
     if (l < Wd) {
-        const size_t base = (size_t)2 * B + 2 * (size_t)B * NA;
-        const size_t o = (size_t)t * Wd + l;
-        const size_t fs = (size_t)B * Wd * N;
+        const size_t r = (size_t)t * Wd + l;
         const float val = i2f(ca.z);  // CNode::value(): 0 when not expanded (stored that way)
         const float rew = i2f(ca.w);
-        if (N == 1)
-            out[base + MZ_F_ACTIONS * fs + o] = has ? act : 0;
-        else
-            for (int i = 0; i < N; ++i) out[base + MZ_F_ACTIONS * fs + o * N + i] = has ? (int)jt[l * N + i] : 0;
-        out[base + MZ_F_VISIT_COUNT * fs + o] = has ? ca.x : 0;
-        fout[base + MZ_F_PRED_PROBS * fs + o] = has ? cd.x : 0.f;
-        fout[base + MZ_F_BETA * fs + o] = has ? cd.y : 0.f;
-        fout[base + MZ_F_BETA_HAT * fs + o] = has ? cd.z : 0.f;
-        fout[base + MZ_F_PRIORS * fs + o] = has ? i2f(ca.y) : 0.f;
-        fout[base + MZ_F_IMP_RATIO * fs + o] = has ? (cd.z / cd.y * cd.x) : 0.f;
-        fout[base + MZ_F_PRED_VALUES * fs + o] = has ? i2f(cb.z) : 0.f;
-        fout[base + MZ_F_MCTS_VALUES * fs + o] = has ? val : 0.f;
-        fout[base + MZ_F_REWARDS * fs + o] = has ? rew : 0.f;
-        fout[base + MZ_F_QVALUES * fs + o] = has ? (rew + disc * val) : 0.f;
+        if (int *fa = o.f[MZ_F_ACTIONS]) {
+            if (N == 1)
+                fa[r] = has ? act : 0;
+            else
+                for (int i = 0; i < N; ++i) fa[r * N + i] = has ? (int)jt[l * N + i] : 0;
+        }
+        if (o.f[MZ_F_VISIT_COUNT]) o.f[MZ_F_VISIT_COUNT][r] = has ? ca.x : 0;
+        const float fv[MZ_F_COUNT] = {0.f, 0.f, cd.x, cd.y, cd.z, i2f(ca.y), cd.z / cd.y * cd.x, i2f(cb.z), val, rew,
+                                      rew + disc * val};
+#pragma unroll
+        for (int f = MZ_F_PRED_PROBS; f < MZ_F_COUNT; ++f)
+            if (o.f[f]) ((float *)o.f[f])[r] = has ? fv[f] : 0.f;
     }
 }
 
@@ -4023,19 +4078,19 @@ void set_lds_limit(int lds) {
     (void)hipFuncSetAttribute((const void *)k_step<false, true, NC, JOINT>, attr, lds);
 }
 
-template <int NC>
+template <int NC, bool SEL = true>
 void launch_chain(mz_batch *b, const StepArgs &a, int lds) {
     const Geo &g = b->geo;
-    hipLaunchKernelGGL((k_chain<NC>), dim3(g.B), dim3(2 * kWave), lds, b->stream, (char *)b->dev.base, g.P, g.PS,
+    hipLaunchKernelGGL((k_chain<NC, SEL>), dim3(g.B), dim3(2 * kWave), lds, b->stream, (char *)b->dev.base, g.P, g.PS,
                        g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value, a.policy, a.beta, a.K, a.hsx,
                        a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy,
                        a.act);
 }
 
-template <int NC>
+template <int NC, bool SEL = true>
 void launch_tree(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
-    hipLaunchKernelGGL((k_tree<NC>), dim3(g.B), dim3(4 * kWave), TreeLayout<NC>::total, b->stream,
+    hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(4 * kWave), TreeLayout<NC>::total, b->stream,
                        (char *)b->dev.base, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value,
                        a.policy, a.beta, a.K, a.hsx, a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes,
                        a.gather_out, a.idx_x, a.idy, a.act);
@@ -4043,16 +4098,27 @@ void launch_tree(mz_batch *b, const StepArgs &a) {
 
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
-    if (eb && sel && b->chain_nc >= 0) {  // K = 1 trees: the chain kernel
-        const bool big = a.pool && a.row_bytes > 4 * 16 * kWave && a.row_bytes <= 16 * 16 * kWave;
+    if (eb && b->chain_nc >= 0) {  // K = 1 trees: the chain kernel
+        const bool big = sel && a.pool && a.row_bytes > 4 * 16 * kWave && a.row_bytes <= 16 * 16 * kWave;
         const int lds = chain_lds_bytes(g.P, b->chain_nc) + (big ? 16 * 16 * kWave : 0);
-        switch (b->chain_nc) {
-            case 64: launch_chain<64>(b, a, lds); break;
-            case 128: launch_chain<128>(b, a, lds); break;
-            case 256: launch_chain<256>(b, a, lds); break;
-            case 512: launch_chain<512>(b, a, lds); break;
-            case 1024: launch_chain<1024>(b, a, lds); break;
-            default: launch_chain<0>(b, a, lds); break;
+        if (sel) {
+            switch (b->chain_nc) {
+                case 64: launch_chain<64>(b, a, lds); break;
+                case 128: launch_chain<128>(b, a, lds); break;
+                case 256: launch_chain<256>(b, a, lds); break;
+                case 512: launch_chain<512>(b, a, lds); break;
+                case 1024: launch_chain<1024>(b, a, lds); break;
+                default: launch_chain<0>(b, a, lds); break;
+            }
+        } else {
+            switch (b->chain_nc) {
+                case 64: launch_chain<64, false>(b, a, lds); break;
+                case 128: launch_chain<128, false>(b, a, lds); break;
+                case 256: launch_chain<256, false>(b, a, lds); break;
+                case 512: launch_chain<512, false>(b, a, lds); break;
+                case 1024: launch_chain<1024, false>(b, a, lds); break;
+                default: launch_chain<0, false>(b, a, lds); break;
+            }
         }
         HIP_TRY(hipGetLastError());
         b->rb_valid = b->rb_dev_valid = false;
@@ -4067,14 +4133,25 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
         const long long pe = b->expansions + 1;
         a.pe = (int)(pe < g.PS ? pe : g.PS);
     }
-    if (eb && sel && b->tree_nc > 0) {  // 2 <= K <= 64 trees: the four-wave kernel
-        switch (b->tree_nc) {
-            case 64: launch_tree<64>(b, a); break;
-            case 128: launch_tree<128>(b, a); break;
-            case 256: launch_tree<256>(b, a); break;
-            case 384: launch_tree<384>(b, a); break;
-            case 512: launch_tree<512>(b, a); break;
-            default: launch_tree<1024>(b, a); break;
+    if (eb && b->tree_nc > 0) {  // 2 <= K <= 64 trees: the four-wave kernel
+        if (sel) {
+            switch (b->tree_nc) {
+                case 64: launch_tree<64>(b, a); break;
+                case 128: launch_tree<128>(b, a); break;
+                case 256: launch_tree<256>(b, a); break;
+                case 384: launch_tree<384>(b, a); break;
+                case 512: launch_tree<512>(b, a); break;
+                default: launch_tree<1024>(b, a); break;
+            }
+        } else {
+            switch (b->tree_nc) {
+                case 64: launch_tree<64, false>(b, a); break;
+                case 128: launch_tree<128, false>(b, a); break;
+                case 256: launch_tree<256, false>(b, a); break;
+                case 384: launch_tree<384, false>(b, a); break;
+                case 512: launch_tree<512, false>(b, a); break;
+                default: launch_tree<1024, false>(b, a); break;
+            }
         }
         HIP_TRY(hipGetLastError());
         b->rb_valid = b->rb_dev_valid = false;
@@ -4113,10 +4190,28 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     return MZ_OK;
 }
 
+// Packed readback layout (4-byte words): [B] root value | [B*NA] marginal visits | [B*NA] marginal
+// priors | [B] degree | MZ_F_COUNT x [B*Wd*N] per-child fields (actions fill [B][Wd][N], the
+// others the first B*Wd words).
+size_t rb_deg_base(const mz_batch *b) { return (size_t)b->B + 2 * (size_t)b->B * b->NA; }
+size_t rb_field_base(const mz_batch *b, int field) {
+    return rb_deg_base(b) + (size_t)b->B + (size_t)field * b->B * b->Wd * b->N;
+}
+size_t rb_field_width(const mz_batch *b, int field) { return (size_t)b->Wd * (field == MZ_F_ACTIONS ? b->N : 1); }
+
+
 // Packed readback computed on the device (stream-ordered, no synchronisation).
 int readback_dev(mz_batch *b, float disc) {
     if (b->rb_dev_valid && b->rb_disc == disc) return MZ_OK;
-    hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, disc, b->Wd, b->rb_dev);
+    RbPtrs o;
+    int *rb = b->rb_dev;
+    const size_t n = (size_t)b->B * b->NA;
+    o.values = (float *)rb;
+    o.mv = rb + b->B;
+    o.mp = (float *)(rb + b->B + n);
+    o.deg = rb + rb_deg_base(b);
+    for (int f = 0; f < MZ_F_COUNT; ++f) o.f[f] = rb + rb_field_base(b, f);
+    hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, disc, b->Wd, o);
     HIP_TRY(hipGetLastError());
     b->rb_dev_valid = true;
     b->rb_valid = false;
@@ -4143,15 +4238,6 @@ int readback(mz_batch *b, float disc) {
     b->rb_valid = true;
     return MZ_OK;
 }
-
-// Packed readback layout (4-byte words): [B] root value | [B*NA] marginal visits | [B*NA] marginal
-// priors | [B] degree | MZ_F_COUNT x [B*Wd*N] per-child fields (actions fill [B][Wd][N], the
-// others the first B*Wd words).
-size_t rb_deg_base(const mz_batch *b) { return (size_t)b->B + 2 * (size_t)b->B * b->NA; }
-size_t rb_field_base(const mz_batch *b, int field) {
-    return rb_deg_base(b) + (size_t)b->B + (size_t)field * b->B * b->Wd * b->N;
-}
-size_t rb_field_width(const mz_batch *b, int field) { return (size_t)b->Wd * (field == MZ_F_ACTIONS ? b->N : 1); }
 
 }  // namespace
 
@@ -4377,12 +4463,12 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         const auto attr = hipFuncAttributeMaxDynamicSharedMemorySize;
         const int tl = tree_lds_bytes(b->tree_nc);
         switch (b->tree_nc) {
-            case 64: (void)hipFuncSetAttribute((const void *)k_tree<64>, attr, tl); break;
-            case 128: (void)hipFuncSetAttribute((const void *)k_tree<128>, attr, tl); break;
-            case 256: (void)hipFuncSetAttribute((const void *)k_tree<256>, attr, tl); break;
-            case 384: (void)hipFuncSetAttribute((const void *)k_tree<384>, attr, tl); break;
-            case 512: (void)hipFuncSetAttribute((const void *)k_tree<512>, attr, tl); break;
-            default: (void)hipFuncSetAttribute((const void *)k_tree<1024>, attr, tl); break;
+            case 64: (void)hipFuncSetAttribute((const void *)k_tree<64, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<64, false>, attr, tl); break;
+            case 128: (void)hipFuncSetAttribute((const void *)k_tree<128, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<128, false>, attr, tl); break;
+            case 256: (void)hipFuncSetAttribute((const void *)k_tree<256, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<256, false>, attr, tl); break;
+            case 384: (void)hipFuncSetAttribute((const void *)k_tree<384, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<384, false>, attr, tl); break;
+            case 512: (void)hipFuncSetAttribute((const void *)k_tree<512, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<512, false>, attr, tl); break;
+            default: (void)hipFuncSetAttribute((const void *)k_tree<1024, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<1024, false>, attr, tl); break;
         }
     }
     if (b->chain_nc >= 0) {
@@ -4390,12 +4476,12 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         if (cl > 64 * 1024) {
             const auto attr = hipFuncAttributeMaxDynamicSharedMemorySize;
             switch (b->chain_nc) {
-                case 64: (void)hipFuncSetAttribute((const void *)k_chain<64>, attr, cl); break;
-                case 128: (void)hipFuncSetAttribute((const void *)k_chain<128>, attr, cl); break;
-                case 256: (void)hipFuncSetAttribute((const void *)k_chain<256>, attr, cl); break;
-                case 512: (void)hipFuncSetAttribute((const void *)k_chain<512>, attr, cl); break;
-                case 1024: (void)hipFuncSetAttribute((const void *)k_chain<1024>, attr, cl); break;
-                default: (void)hipFuncSetAttribute((const void *)k_chain<0>, attr, cl); break;
+                case 64: (void)hipFuncSetAttribute((const void *)k_chain<64, true>, attr, cl); (void)hipFuncSetAttribute((const void *)k_chain<64, false>, attr, cl); break;
+                case 128: (void)hipFuncSetAttribute((const void *)k_chain<128, true>, attr, cl); (void)hipFuncSetAttribute((const void *)k_chain<128, false>, attr, cl); break;
+                case 256: (void)hipFuncSetAttribute((const void *)k_chain<256, true>, attr, cl); (void)hipFuncSetAttribute((const void *)k_chain<256, false>, attr, cl); break;
+                case 512: (void)hipFuncSetAttribute((const void *)k_chain<512, true>, attr, cl); (void)hipFuncSetAttribute((const void *)k_chain<512, false>, attr, cl); break;
+                case 1024: (void)hipFuncSetAttribute((const void *)k_chain<1024, true>, attr, cl); (void)hipFuncSetAttribute((const void *)k_chain<1024, false>, attr, cl); break;
+                default: (void)hipFuncSetAttribute((const void *)k_chain<0, true>, attr, cl); (void)hipFuncSetAttribute((const void *)k_chain<0, false>, attr, cl); break;
             }
         }
     }
@@ -4472,7 +4558,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     }
     a.eps = noise_eps;
     a.K = K;
-    hipLaunchKernelGGL(k_set_word, dim3(1), dim3(1), 0, b->stream, (unsigned *)b->dev.err(), 0u);
+    a.idx_x = a.idy = a.act = nullptr;
     const size_t jl = (b->N > 1) ? (size_t)((12 * b->NA + 15) & ~15) + 8 * (size_t)b->NA + 4 * (size_t)kWave * b->N : 0;
     hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), jl, b->stream, b->prm, a);
     HIP_TRY(hipGetLastError());
@@ -4480,6 +4566,40 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     b->prepared = true;
     b->expansions = 1;
     if (mem == MZ_MEM_HOST) return check_device_errors(b);
+    return MZ_OK;
+}
+
+int mz_prepare_select(mz_batch *b, const float *rewards, const float *values, const float *policy, const float *beta,
+                      int K, float noise_eps, const float *noises, float c2, float c1, float discount, int32_t *idx_x,
+                      int32_t *idy, int32_t *actions) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
+    if (!idx_x || !idy || !actions) return fail(MZ_ERR_ARG, "null selection output");
+    if (b->N > 1) {  // joint-action trees: the two calls
+        int rc = mz_prepare(b, rewards, values, policy, beta, K, noise_eps, noises, MZ_MEM_DEVICE);
+        if (rc) return rc;
+        return mz_select(b, c2, c1, discount, idx_x, idy, actions, MZ_MEM_DEVICE);
+    }
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = ensure_tables(b, c2, c1);  // (for the launches that follow; the first selection needs none)
+    if (rc) return rc;
+    PrepArgs a;
+    a.reward = rewards;
+    a.value = values;
+    a.policy = policy;
+    a.beta = beta;
+    a.noise = noises;
+    a.eps = noise_eps;
+    a.K = K;
+    a.idx_x = idx_x;
+    a.idy = idy;
+    a.act = actions;
+    hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), 0, b->stream, b->prm, a);
+    HIP_TRY(hipGetLastError());
+    b->rb_valid = b->rb_dev_valid = false;
+    b->prepared = true;
+    b->expansions = 1;
     return MZ_OK;
 }
 
@@ -4631,6 +4751,22 @@ int mz_gather_rows(mz_batch *b, const void *pool, int64_t stride, int64_t row_by
     if (rc) return rc;
     hipLaunchKernelGGL(k_gather, dim3(b->B), dim3(kWave), 0, b->stream, (const char *)pool, (long long)stride,
                        (long long)row_bytes, (const int *)idx_x, (char *)out);
+    HIP_TRY(hipGetLastError());
+    return MZ_OK;
+}
+
+int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    if (!out) return fail(MZ_ERR_ARG, "null output list");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    RbPtrs o;
+    o.values = out->values;
+    o.mv = out->marginal_visit_count;
+    o.mp = out->marginal_priors;
+    o.deg = out->degrees;
+    for (int f = 0; f < MZ_F_COUNT; ++f) o.f[f] = (int *)out->sampled[f];
+    hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, discount, b->Wd, o);
     HIP_TRY(hipGetLastError());
     return MZ_OK;
 }

@@ -22,7 +22,7 @@ import ctypes as C
 import numpy as np
 
 from . import _capi
-from ._capi import FIELDS, INT_FIELDS, MZ_MEM_DEVICE, MZ_MEM_HOST, check
+from ._capi import FIELDS, INT_FIELDS, MZ_MEM_DEVICE, MZ_MEM_HOST, ReadbackOut, check
 
 try:  # torch is plumbing for device memory/streams; the host path works without it
     import torch
@@ -190,6 +190,21 @@ class Tree_batch:
         check(self._lib, rc, "batch_selection_device")
         return out
 
+    def prepare_selection_device(self, rewards, values, policy_probs, beta, sampled_times, noise_eps, noises,
+                                 pb_c_base, pb_c_init, discount, out):
+        """prepare + batch_selection_device in one launch (include/mzmcts.h mz_prepare_select): the
+        first selection after prepare is the root's forced first child (cnode.cpp:398-399)."""
+        ts = [_f32_dev(t) for t in (rewards, values, policy_probs, beta, noises)]
+        self._sync_stream()
+        rc = self._lib.mz_prepare_select(
+            self._h, *[C.c_void_p(t.data_ptr()) for t in ts[:4]], int(sampled_times), float(noise_eps),
+            C.c_void_p(ts[4].data_ptr()), float(pb_c_base), float(pb_c_init), float(discount),
+            C.c_void_p(out[0].data_ptr()), C.c_void_p(out[1].data_ptr()), C.c_void_p(out[2].data_ptr()),
+        )
+        check(self._lib, rc, "prepare_selection_device")
+        self._maxdeg = None
+        return out
+
     def expansion_backup_selection_device(self, hidden_state_index_x, discount, sampled_times, rewards, values,
                                           policy_probs, beta, pb_c_base, pb_c_init, out, pool=None,
                                           gather_out=None):
@@ -255,6 +270,20 @@ class Tree_batch:
         check(self._lib, self._lib.mz_get_roots_marginal_priors(self._h, C.c_void_p(prior_out.data_ptr()),
                                                                  MZ_MEM_DEVICE), "marginal_priors_device")
         return visit_out, prior_out
+
+    def get_roots_device(self, discount: float = 0.0, values=None, marginal_visit_count=None, marginal_priors=None,
+                         degrees=None, sampled=None):
+        """Every requested readback of all roots in ONE launch, written into the given device tensors
+        (include/mzmcts.h mz_get_roots_device): values [B] f32, marginal_* [B, N, A], degrees [B] int32,
+        sampled {field name: [B, max_children(*N)]} as get_roots_sampled_padded_device lays them out."""
+        o = ReadbackOut()
+        ptr = lambda x: None if x is None else x.data_ptr()  # noqa: E731
+        o.values, o.marginal_visit_count = ptr(values), ptr(marginal_visit_count)
+        o.marginal_priors, o.degrees = ptr(marginal_priors), ptr(degrees)
+        for name, t in (sampled or {}).items():
+            o.sampled[FIELDS[name]] = t.data_ptr()
+        self._sync_stream()
+        check(self._lib, self._lib.mz_get_roots_device(self._h, float(discount), C.byref(o)), "get_roots_device")
 
     def get_roots_sampled_padded_device(self, name: str, discount: float = 0.0, degrees_out=None):
         """Device form of get_roots_sampled_padded: (tensor [B, maxdeg(*N)], degrees int32 [B])."""

@@ -34,7 +34,7 @@ from typing import List, NamedTuple, Tuple
 import numpy as np
 import torch
 
-from ._capi import MZ_DT_F16, MZ_DT_F32, check
+from ._capi import INT_FIELDS, MZ_DT_F16, MZ_DT_F32, check
 from .cytree import Tree_batch
 
 
@@ -141,9 +141,9 @@ class _SearchLoop:
         c2, c1, disc = cfg.pb_c_base, cfg.pb_c_init, cfg.discount
         K, S = cfg.sampled_action_times, cfg.num_simulations
         r = self.rin
-        tb.prepare(r[0], r[1], r[2], r[3], K, eps, r[4])
         model.eval()
-        tb.batch_selection_device(c2, c1, disc, out=self.sel)
+        # prepare + the first selection (the root's forced first child) in one launch
+        tb.prepare_selection_device(r[0], r[1], r[2], r[3], K, eps, r[4], c2, c1, disc, out=self.sel)
         act = self.sel[2]
         leaf = self.root  # simulation 0 selects a child of every root: its parent is the root (slot 0)
         for s in range(S):
@@ -354,12 +354,17 @@ class SampledMCTS:
                     tb.get_roots_sampled_priors(), tb.get_roots_sampled_imp_ratio(),
                     tb.get_roots_sampled_pred_values(), tb.get_roots_sampled_mcts_values(),
                     tb.get_roots_sampled_rewards(), tb.get_roots_sampled_qvalues(disc))
-            value = tb.get_roots_values_device()
-            mv, mp = tb.get_roots_marginal_device()
+            # every output in one readback launch (mz_get_roots_device)
+            W, Nt = tb.max_children(), tb.agent_num  # (the trees' agent_num, mcts_sampled.py:89)
+            value = torch.empty(B, dtype=torch.float32, device=dev)
+            mv = torch.empty(B, Nt, A, dtype=torch.int32, device=dev)
+            mp = torch.empty(B, Nt, A, dtype=torch.float32, device=dev)
             deg = torch.empty(B, dtype=torch.int32, device=dev)
-            sampled = {}
-            for f in _SAMPLED_FIELDS:
-                sampled[f], _ = tb.get_roots_sampled_padded_device(f, disc, degrees_out=deg if f == "actions" else None)
+            sampled = {f: torch.empty(B, W * Nt if f == "actions" else W,
+                                      dtype=torch.int32 if f in INT_FIELDS else torch.float32, device=dev)
+                       for f in _SAMPLED_FIELDS}
+            tb.get_roots_device(disc, values=value, marginal_visit_count=mv, marginal_priors=mp, degrees=deg,
+                                sampled=sampled)
             return DeviceSearchOutput(value, mv, mp, deg, sampled, tb)
 
     @staticmethod

@@ -438,6 +438,13 @@ int mz_expand_backup_select(mz_batch *, int, float, int, const float *, const fl
                             const void *, int64_t, int64_t, void *) {
     return fail(MZ_ERR_UNSUPPORTED, "cpu port: fused device path not available");
 }
+int mz_prepare_select(mz_batch *, const float *, const float *, const float *, const float *, int, float,
+                      const float *, float, float, float, int32_t *, int32_t *, int32_t *) {
+    return fail(MZ_ERR_UNSUPPORTED, "cpu port: fused device path not available");
+}
+int mz_get_roots_device(mz_batch *, float, const mz_readback_out *) {
+    return fail(MZ_ERR_UNSUPPORTED, "cpu port: device readbacks not available");
+}
 int mz_gather_rows(mz_batch *, const void *, int64_t, int64_t, const int32_t *, void *) {
     return fail(MZ_ERR_UNSUPPORTED, "cpu port: device gather not available");
 }

@@ -381,3 +381,55 @@ def test_joint_action_trees_vs_port(gpu_lib, port_lib, name, B, N, A, K, S):
             assert g.shape == c.shape, (k, i)
             np.testing.assert_array_equal(g.view(np.int32), c.view(np.int32), err_msg=f"{k}[{i}]")
     assert (out_g["mv"].sum(axis=2) == S).all()  # every agent's marginal sums to the simulations
+
+
+@pytest.mark.parametrize("K", [1, 5])
+def test_prepare_select_and_one_launch_readback(gpu_lib, port_lib, K):
+    """mz_prepare_select (prepare + the first selection in one launch) and mz_get_roots_device (every
+    readback in one launch) against the separate calls of the CPU port, at a BASELINE-like size."""
+    from mazero_amd.synthetic import DEFAULTS, make_search_inputs, readbacks
+
+    B, A, S = 128, 9, 30
+    inp = make_search_inputs(np.random.default_rng(40 + K), B, A, S)
+    c2, c1, g = DEFAULTS["pb_c_base"], DEFAULTS["pb_c_init"], DEFAULTS["discount"]
+    ref = make_tb(port_lib, inp, K, {})
+    ref.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps, inp.root_noise)
+    ref_sel = [ref.batch_selection(c2, c1, g)]
+    for s in range(S - 1):
+        ref.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+        ref_sel.append(ref.batch_selection(c2, c1, g))
+    dinp = to_device(inp)
+    tb = make_tb(gpu_lib, inp, K, {})
+    dev = torch.device("cuda")
+    out = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev),
+           torch.empty(B, 1, dtype=torch.int32, device=dev))
+    tb.prepare_selection_device(dinp.root_reward, dinp.root_value, dinp.root_policy, dinp.root_beta, K,
+                                dinp.noise_eps, dinp.root_noise, c2, c1, g, out=out)
+    got = [(out[0].cpu().tolist(), out[1].cpu().tolist(), out[2].cpu().numpy())]
+    for s in range(S - 1):
+        tb.expansion_backup_selection_device(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s],
+                                             dinp.beta[s], c2, c1, out=out)
+        got.append((out[0].cpu().tolist(), out[1].cpu().tolist(), out[2].cpu().numpy()))
+    for s, ((gi, gy, ga), (ri, ry, ra)) in enumerate(zip(got, ref_sel)):
+        assert gi == list(ri) and gy == list(ry), f"selection {s}"
+        assert np.array_equal(ga.reshape(B, -1), np.asarray(ra).reshape(B, -1)), f"actions {s}"
+    # every field of one mz_get_roots_device launch == the per-field readbacks of the port
+    from mazero_amd._capi import FIELDS, INT_FIELDS
+
+    exp = readbacks(ref, g)
+    W = tb.max_children()
+    vals = torch.empty(B, device=dev)
+    mv = torch.empty(B, 1, A, dtype=torch.int32, device=dev)
+    mp = torch.empty(B, 1, A, device=dev)
+    deg = torch.empty(B, dtype=torch.int32, device=dev)
+    sampled = {f: torch.zeros(B, W, dtype=torch.int32 if f in INT_FIELDS else torch.float32, device=dev) for f in FIELDS}
+    tb.get_roots_device(g, values=vals, marginal_visit_count=mv, marginal_priors=mp, degrees=deg, sampled=sampled)
+    torch.cuda.synchronize()
+    assert np.array_equal(vals.cpu().numpy().view(np.int32), exp["root_values"].view(np.int32))
+    assert np.array_equal(mv.cpu().numpy(), exp["marginal_visit_count"])
+    assert np.array_equal(mp.cpu().numpy().view(np.int32), np.asarray(exp["marginal_priors"], np.float32).view(np.int32))
+    assert np.array_equal(deg.cpu().numpy(), exp["degree"])
+    for f, t_ in sampled.items():
+        e = exp["sampled_" + f]
+        gg = t_.cpu().numpy()[:, : e.shape[1]]
+        assert np.array_equal(gg.view(np.int32), e.astype(gg.dtype).view(np.int32)), f
