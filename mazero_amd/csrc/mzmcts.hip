@@ -42,6 +42,7 @@
 #include "../../include/mzmcts.h"
 #include "../../include/mzdriver.h"
 #include "mz_internal.h"
+#include "mt_seed.inc"
 
 namespace {
 
@@ -790,6 +791,32 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     // error also stays in its header, and every later kernel re-reports the errors of dead trees,
     // so an error raised by another block before this store is not lost.
     if (t == 0 && tid == 0) *d.err() = 0;
+#ifndef MZ_SEED_LOOP
+    if (tid < kWave) {
+        // std::mt19937::seed (sequential by definition) on the scalar unit: 4 SALU operations per
+        // word, word i into lane i % 64 of VGPR i / 64 (mt_seed.inc, scripts/gen_mt_seed.py), then
+        // ten LDS stores.  Replaces a compiler loop of ~6.5 instructions per word (10.4 us -> ...)
+        unsigned x = (unsigned)__builtin_amdgcn_readfirstlane((int)(d.seed()[0] * 2333u + (unsigned)(g.root_offset + t)));
+        unsigned tt;
+        int v0 = (int)x, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0, v6 = 0, v7 = 0, v8 = 0, v9 = 0;
+        asm volatile(MZ_MT_SEED_ASM
+                     : [x] "+s"(x), [t] "=&s"(tt), [v0] "+v"(v0), [v1] "+v"(v1), [v2] "+v"(v2), [v3] "+v"(v3),
+                       [v4] "+v"(v4), [v5] "+v"(v5), [v6] "+v"(v6), [v7] "+v"(v7), [v8] "+v"(v8), [v9] "+v"(v9)
+                     :
+                     : "scc");
+        const int l = tid;
+        mt[l] = (unsigned)v0;
+        mt[64 + l] = (unsigned)v1;
+        mt[128 + l] = (unsigned)v2;
+        mt[192 + l] = (unsigned)v3;
+        mt[256 + l] = (unsigned)v4;
+        mt[320 + l] = (unsigned)v5;
+        mt[384 + l] = (unsigned)v6;
+        mt[448 + l] = (unsigned)v7;
+        mt[512 + l] = (unsigned)v8;
+        if (576 + l < kMtN) mt[576 + l] = (unsigned)v9;
+    }
+#else
     if (tid == 0) {  // std::mt19937::seed: sequential by definition
         unsigned x = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
         mt[0] = x;
@@ -798,8 +825,12 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
             mt[i] = x;
         }
     }
+#endif
     __syncthreads();
-    const int nb = g.W / kMtN;
+    int nb = g.W / kMtN;
+#ifdef MZ_ABL_NOTWIST  // ablation (timing experiments only): no twist / tempering
+    nb = 0;
+#endif
     for (int blk = 0; blk < nb; ++blk) {
         unsigned v = 0;
         // k in [0, 227): x[k] = x[k+397] ^ twist(x[k], x[k+1])       (all old)
