@@ -2349,7 +2349,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
 // --------------------------------------------------------------------------------------------
 template <int NC>  // node capacity class (P = S + 2 <= NC); 0: offsets from P at run time
 struct ChainLayout {
-    int oA, oC, oPP, oLp, oR, oBoot, oW, oP, total;
+    int oA, oC, oPP, oLp, oR, oBoot, oW, oP, oPol, oLb, oSt, total;
     __host__ __device__ static constexpr int r16(int x) { return (x + 15) & ~15; }
     __host__ __device__ constexpr ChainLayout(int P)
         : oA(0),
@@ -2360,7 +2360,10 @@ struct ChainLayout {
           oBoot(oR + r16(4 * (P + kWave))),
           oW(oBoot + r16(4 * (P + kWave))),
           oP(oW + r16(4 * kMaxActions)),
-          total(oP + r16(8 * kMaxActions)) {}
+          oPol(oP + r16(8 * kMaxActions)),
+          oLb(oPol + r16(4 * kMaxActions)),
+          oSt(oLb + 16),
+          total(oSt + r16(8 * kWave)) {}
 };
 template <int NC>
 __device__ __forceinline__ ChainLayout<NC> chain_layout(int P) {
@@ -2487,6 +2490,8 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     const int l = threadIdx.x & (kWave - 1);
     const int wv = uni((int)(threadIdx.x >> 6));
     const size_t nb = (size_t)t * P;
+    unsigned long long ts[8] = {0};
+    stamp(ts, 0);
     // ---- round 1: everything, from the arguments (the chain's length is hsx) ----
     int Dp = hsx;  // back-propagation path 0..Dp, leaf Dp, tot = Dp + 1
     if (Dp < 0 || Dp + 1 > P) Dp = 0;
@@ -2501,37 +2506,40 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     const bool g_reg = row_al && row_bytes <= 4 * 16 * kWave;
     const bool g_lds = row_al && !g_reg && row_bytes <= 16 * 16 * kWave;
     int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+    // Round 1 is LDS-DMA and scalar loads (invisible to the compiler's wait counting) plus, last,
+    // the leaf row's loads: the counted wait below leaves exactly those in flight until the end.
+    float *sPol = (float *)(smem + L.oPol);
+    float *sW = (float *)(smem + L.oW);
+    long long *sSt = (long long *)(smem + L.oSt);
     if (wv == 0) {
         for (int i0 = 0; i0 <= Dp; i0 += kWave)
             if (i0 + l <= Dp) {
-                glds16(d.A() + nb + i0 + l, sA + i0);
-                glds16(d.C() + nb + i0 + l, sC + i0);
-                glds4(d.PP() + nb + i0 + l, sPP + i0);
-                glds4(d.lp() + i0 + l, sLp + i0);
+                glds16a(d.A() + nb + i0 + l, sA + i0);
+                glds16a(d.C() + nb + i0 + l, sC + i0);
+                glds4a(d.PP() + nb + i0 + l, sPP + i0);
+                glds4a(d.lp() + i0 + l, sLp + i0);
             }
-        const size_t ib = (size_t)t * A;
-        if (l < A) {
-            pol = policy[ib + l];
-            bet = beta[ib + l];
-        }
-        if (l < MZ_S_CYC_HEADER) st_old = (unsigned long long)st[l];
-        leaf_b = d.Bn()[nb + Dp];
+        const size_t ib = (size_t)t * A + (l < A ? l : 0);
+        glds4a(policy + ib, sPol);
+        glds4a(beta + ib, sW);  // (lanes >= A: zero weights, below)
+        glds4a((const int *)st + (l < 2 * MZ_S_COUNT ? l : 0), (int *)sSt);
+        if (l == 0) glds16a(d.Bn() + nb + Dp, smem + L.oLb);
         if (g_reg || g_lds) {
             const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
             const long long last = row_bytes - 16, o = (long long)l * 16;
-            if (g_reg) {
+            if (g_reg) {  // always four loads (offsets clamped into the row)
                 gv0 = *(const int4 *)(src + (o < last ? o : last));
                 gv1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
                 gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
                 gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
-            } else {
+            } else {  // always sixteen chunks
 #pragma unroll
-                for (int k = 0; k < 16; ++k) glds16(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+                for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
             }
         }
     } else {
         for (int i0 = 0; i0 <= Dp; i0 += kWave)
-            if (i0 + l <= Dp) glds4(&d.A()[nb + i0 + l].w, sR + i0);
+            if (i0 + l <= Dp) glds4a(&d.A()[nb + i0 + l].w, sR + i0);
     }
     // the header, the leaf's structure record and the network outputs of this tree (scalar loads)
     TreeHdr h;
@@ -2546,13 +2554,23 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
         h.nxt[0] = hp->nxt[0];
         h.nxt[1] = hp->nxt[1];
     }
-    const float r_in = reward[t], v_in = value[t];
+    const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
     const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
     const int gW = pl->g.W;
     const float omr = pl->g.one_minus_rho;
     const unsigned oR = pl->d.o_R;
     d.o_D = pl->d.o_D;
-    wait_vm();
+    if (wv == 0 && g_reg) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");        // the row stays in flight
+    else if (wv == 0 && g_lds) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // (its chunks too)
+    else wait_vm();
+    if (wv == 0) {
+        if (l >= A) sW[l] = 0.f;
+        pol = sPol[l < A ? l : 0];
+        bet = sW[l < A ? l : 0];
+        if (l < ((MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER)) st_old = (unsigned long long)sSt[l];
+        leaf_b = *(const int4 *)(smem + L.oLb);
+    }
+    stamp(ts, 1);
     if (h.err) {  // a dead tree stays dead (both waves see the same header) and re-reports its error
         if (wv == 0) {
             if (l == 0) {
@@ -2564,6 +2582,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
                 atomicOr(d.err(), h.err);
             }
         }
+        wait_vm();  // (the row's loads / chunks)
         return;
     }
     // a graph replayed out of sequence: the header's chain, not the arguments' (both waves)
@@ -2580,21 +2599,23 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
                 hp->err = kErrPath;
                 atomicOr(d.err(), kErrPath);
             }
+            wait_vm();
             return;
         }
         for (int i0 = 0; i0 <= D; i0 += kWave)
             if (i0 + l <= D) {
                 if (wv == 0) {
-                    glds16(d.A() + nb + i0 + l, sA + i0);
-                    glds16(d.C() + nb + i0 + l, sC + i0);
-                    glds4(d.PP() + nb + i0 + l, sPP + i0);
-                    glds4(d.lp() + i0 + l, sLp + i0);
+                    glds16a(d.A() + nb + i0 + l, sA + i0);
+                    glds16a(d.C() + nb + i0 + l, sC + i0);
+                    glds4a(d.PP() + nb + i0 + l, sPP + i0);
+                    glds4a(d.lp() + i0 + l, sLp + i0);
                 } else {
-                    glds4(&d.A()[nb + i0 + l].w, sR + i0);
+                    glds4a(&d.A()[nb + i0 + l].w, sR + i0);
                 }
             }
-        if (wv == 0) leaf_b = d.Bn()[nb + D];
+        if (wv == 0 && l == 0) glds16a(d.Bn() + nb + D, smem + L.oLb);
         wait_vm();
+        if (wv == 0) leaf_b = *(const int4 *)(smem + L.oLb);
     }
 
     if (wv == 1) {
@@ -2616,6 +2637,11 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
             carry = rlf(b, 63 - nl);
             hi = lo;
         }
+        if (MZ_STAMPS) {
+            wait_lds();
+            stamp(ts, 2);
+            if (l == 0) *(unsigned long long *)(smem + L.oR) = ts[2] - ts[1];  // (wave 1: the chain; sR[0..1] are free now)
+        }
         lds_barrier();
         return;
     }
@@ -2634,6 +2660,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
         cursor += 2;
     }
     a = uni(a);
+    stamp(ts, 2);
     if (c + 1 > P) err |= kErrPool;
     const float bh = 1.0f;  // betahat_prob = count / sampled_times = 1 / 1
     const float pol_a = rlf(pol, a), bet_a = rlf(bet, a);
@@ -2669,7 +2696,9 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     if (value_lim(1, omr) != 1) err |= kErrValueSet;  // (count 1: size_lim must be 1, utils.cpp:31)
 
     // ---- CTree::back_propagate (cnode.cpp:415-450) over the chain, lane i = node i ----
+    stamp(ts, 3);
     lds_barrier();  // the bootstrap values
+    stamp(ts, 4);
     float mn = INFINITY, mx = -INFINITY;
     for (int i0 = 0; i0 <= D; i0 += kWave) {
         const int i = i0 + l;
@@ -2698,6 +2727,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     // min / max over the q of the visited non-root nodes: the whole chain 1..D
     mn = unif(rlf(wave_min_to63(mn), 63));
     mx = unif(rlf(wave_max_to63(mx), 63));
+    stamp(ts, 5);
     const int mm_cnt = D;
 
     if (SEL && !fast && !err) {
@@ -2742,6 +2772,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     }
 
     // ---- outputs (mcts_sampled.py:123-134), the header, the statistics ----
+    stamp(ts, 6);
     if (SEL && l == 0) {
         idx_x[t] = err ? 0 : hsx;  // parent->hidden_state_index_x: the expanded leaf's
         idy[t] = t;
@@ -2780,9 +2811,20 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
             hp->leaf = (err || !SEL) ? h.leaf : c;
         }
     }
-    if (l < MZ_S_CYC_HEADER) {
+    stamp(ts, 7);
+    constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
+    if (l < kStatN) {
         long long add = 0;
         switch (l) {
+            case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;   // round 1
+            case MZ_S_CYC_EXP_CDF: add = (long long)(ts[2] - ts[1]); break;  // distribution + draw
+            case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;   // child, header words
+            case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;   // wait for the chain
+            case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;   // node updates + min/max
+            case MZ_S_CYC_SELECT: add = (long long)(ts[6] - ts[5]); break;   // selection
+            case MZ_S_CYC_EPILOGUE: add = (long long)(ts[7] - ts[6]); break; // outputs, header
+            case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? *(const long long *)(smem + L.oR) : 0; break;
+            case MZ_S_STAMPED: add = 1; break;
             case MZ_S_SELECTS: add = SEL ? 1 : 0; break;
             case MZ_S_PATH_EDGES: add = SEL ? Ds : 0; break;
             case MZ_S_SCORED: add = SEL ? Ds : 0; break;
