@@ -3544,6 +3544,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     unsigned long long tp[4] = {0};
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
     long long nscored = 0;
+    int px = 0, pvv = 0;  // level i's node (and, by levels, its visits) in lane i; sPath past 64 levels
     if constexpr (!SEL) {
         stamp(ts, 5);
     } else if constexpr (kTreeLevels<NC>) {
@@ -3556,7 +3557,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
             const float delta = mmx - mmn;
             den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
         }
-        int px = 0, pvv = 0;
         int xv = uni(sA[0].x) + 1;  // the root is on every path
         int4 xb = uni4(sB[0]);
         int par_hsx = xb.w;
@@ -3657,11 +3657,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
             }
         }
         if (Dn == 0) err |= kErrRoot;
-        wait_lds();
-        // the path {node, visits at selection} for the next back-propagation
-        int2 *gp = d.path() + (size_t)t * PS;
-        for (int i0 = 0; i0 <= Dn; i0 += kWave)
-            if (i0 + l <= Dn) gp[i0 + l] = (i0 == 0) ? make_int2(px, pvv) : sPath[i0 + l];
         out_idx = (Dn == 0) ? uni(sB[0].w) : par_hsx;  // parent->hidden_state_index_x
         out_act = act_of(uni(xb.y));                   // children_action of the last edge
     }
@@ -3674,8 +3669,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         const int *nxt = (const int *)(smem + L::oPar);
         const float2 *rec = (const float2 *)(smem + L::oAz);
         cursor = uni(cursor);
-        int px = 0;
-        int v;
+        int v, xprev = 0;
         {
             const int4 r0b = uni4(sB[0]);
             const int rv = uni(sA[0].x) + 1;  // the root is on every path
@@ -3726,6 +3720,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 err |= kErrPath;
                 break;
             }
+            xprev = x;
             x = v;
             ++Dn;
             if (Dn < kWave) px = wl(px, x, Dn);
@@ -3735,25 +3730,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         }
         if (cursor > gW) err |= kErrRng;  // a consumed word beyond the stream
         if (Dn == 0) err |= kErrRoot;
-        wait_lds();
-        // the path {node, visits at selection} for the next back-propagation, the scored children
-        // and the outputs, by the whole wave
-        int2 *gp = d.path() + (size_t)t * PS;
-        int nsc = 0, xpar = 0;
-        for (int i0 = 0; i0 <= Dn; i0 += kWave) {
-            const int i = i0 + l;
-            if (i <= Dn) {
-                const int xi_ = (i < kWave) ? px : sPath[i].x;
-                const int vis = sA[xi_].x + (sFl[xi_] ? 1 : 0);
-                gp[i] = make_int2(xi_, vis);
-                const int4 bi = sB[xi_];
-                if (i < Dn && !(i == 0 && vis <= nc_of(bi.y))) nsc += nc_of(bi.y);  // scored levels
-                if (i == Dn - 1) xpar = bi.w;
-            }
-        }
-        nscored = wave_sum(nsc);
-        out_idx = (Dn == 0) ? uni(sB[0].w) : uni(rl(xpar, (Dn - 1) & (kWave - 1)));  // parent->hidden_state_index_x
-        out_act = act_of(uni(sB[x].y));                                             // children_action of the last edge
+        out_idx = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
+        out_act = act_of(uni(sB[x].y));            // children_action of the last edge
     }
     }
     stamp(ts, 6);
@@ -3762,27 +3740,22 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         idy[t] = t;
         act[t] = err ? 0 : out_act;
     }
-    // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[idx_x][t]
-    int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
-    bool gath_reg = false, gath_lds = false;
+    // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[idx_x][t].  Rows up to 16 KiB go
+    // through LDS-DMA into the value-entry area (free once wave 1 is done), so nothing waits for
+    // them until the copy-out at the very end
+    bool gath_lds = false;
     char *gdst = nullptr;
-    unsigned char *sbig = smem + L::oReg;  // (wave 1's value entries are done)
+    unsigned char *sbig = smem + L::oReg;
     if (SEL && pool && !err) {
         const char *src = pool + (long long)out_idx * pool_stride + (long long)t * row_bytes;
         gdst = gather_out + (long long)t * row_bytes;
         const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) &
                          15) == 0;
         const long long o = (long long)l * 16;
-        if (al && row_bytes <= 4 * 16 * kWave) {
-            if (o < row_bytes) gv0 = *(const int4 *)(src + o);
-            if (o + 1024 < row_bytes) gv1 = *(const int4 *)(src + o + 1024);
-            if (o + 2048 < row_bytes) gv2 = *(const int4 *)(src + o + 2048);
-            if (o + 3072 < row_bytes) gv3 = *(const int4 *)(src + o + 3072);
-            gath_reg = true;
-        } else if (al && row_bytes <= 16 * 16 * kWave && row_bytes <= 8ll * kRegCap) {
+        if (al && row_bytes <= 16 * 16 * kWave && row_bytes <= 8ll * kRegCap) {
             const long long last = row_bytes - 16;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+            for (int k = 0; 1024ll * k < row_bytes; ++k)
+                glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
             gath_lds = true;
         } else if (al) {
             for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(gdst + o2) = *(const int4 *)(src + o2);
@@ -3791,13 +3764,42 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 *(int *)(gdst + o2) = *(const int *)(src + o2);
         }
     }
+    if (SEL && !err) {
+        // the path {node, visits at selection} for the next back-propagation (and the scored
+        // children), while the row's loads are in flight
+        wait_lds();
+        int2 *gp = d.path() + (size_t)t * PS;
+        int nsc = 0;
+        for (int i0 = 0; i0 <= Dn; i0 += kWave) {
+            const int i = i0 + l;
+            if (i <= Dn) {
+                const int xi_ = (i < kWave) ? px : sPath[i].x;
+                if constexpr (kTreeLevels<NC>) {
+                    gp[i] = (i < kWave) ? make_int2(xi_, pvv) : sPath[i];
+                } else {
+                    const int vis = sA[xi_].x + (sFl[xi_] ? 1 : 0);
+                    gp[i] = make_int2(xi_, vis);
+                    const int nci = nc_of(sB[xi_].y);
+                    if (i < Dn && !(i == 0 && vis <= nci)) nsc += nci;  // scored levels
+                }
+            }
+        }
+        if constexpr (!kTreeLevels<NC>) nscored = wave_sum(nsc);
+    }
     stamp(ts, 7);
     {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
         const int cur = err ? h.cursor : cursor;
-        const int o = cur + l - wbase;
+        const int o0 = cur - wbase;
         TreeHdr *hp = d.hdr() + t;
-        if (l < kNxt)
-            hp->nxt[l] = (o >= 0 && o < kRngWin) ? sRng[o] : ((cur + l < gW) ? d.R()[(size_t)t * gW + cur + l] : 0u);
+        if (uni((int)(o0 >= 0 && o0 + kNxt <= kRngWin))) {
+            if (l < kNxt) hp->nxt[l] = sRng[o0 + l];
+        } else {  // beyond the window (rare): through LDS-DMA (no compiler wait on the row's loads)
+            unsigned *scr = (unsigned *)(smem + L::oIx);
+            const int w = cur + l < gW ? cur + l : gW - 1;
+            glds4a(d.R() + (size_t)t * gW + w, scr);
+            wait_vm();
+            if (l < kNxt) hp->nxt[l] = (cur + l < gW) ? scr[l] : 0u;
+        }
         if (l == 0) {
             hp->cursor = cur;
             hp->tot = err ? h.tot : ntot;
@@ -3813,13 +3815,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     if (gath_lds) {
         wait_vm();
         for (long long o = (long long)l * 16; o < row_bytes; o += 16 * kWave) *(int4 *)(gdst + o) = *(const int4 *)(sbig + o);
-    }
-    if (gath_reg) {
-        const long long o = (long long)l * 16;
-        if (o < row_bytes) *(int4 *)(gdst + o) = gv0;
-        if (o + 1024 < row_bytes) *(int4 *)(gdst + o + 1024) = gv1;
-        if (o + 2048 < row_bytes) *(int4 *)(gdst + o + 2048) = gv2;
-        if (o + 3072 < row_bytes) *(int4 *)(gdst + o + 3072) = gv3;
     }
     stamp(ts, 8);
     if (l < kStatN) {
