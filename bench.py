@@ -247,8 +247,7 @@ class HipLeg:
         achieved = bytes_per_launch / avg / 1e9
         pmc = pmc_traffic(self.args)
         r = dict(
-            kernel=("k_chain (K = 1 fused expand+backup+select+gather)" if K == 1 else
-                    "k_step<true,true> (fused expand+backup+select+gather)"),
+            kernel=fused_kernel_name(K, K * (S + 2)),
             bound="hbm",
             achieved=round(achieved, 3),
             peak=8000.0,
@@ -266,6 +265,16 @@ class HipLeg:
             # diagnostic build: average shader cycles per fused launch and tree, per phase
             r["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
         return r
+
+
+def fused_kernel_name(K: int, P: int) -> str:
+    """The per-simulation fused kernel the library launches for sampled_times K and a pool of P
+    nodes (launch_step in mazero_amd/csrc/mzmcts.hip)."""
+    if K == 1:
+        return "k_chain (K = 1 chains: fused expand+backup+select+gather)"
+    if 2 <= K <= 64 and P <= 1024:
+        return "k_tree (four waves: fused expand+backup+select+gather)"
+    return "k_step<true,true> (fused expand+backup+select+gather)"
 
 
 class PortLeg:
