@@ -6,8 +6,10 @@ after another (core/selfplay_worker.py:196-211), each search = prepare + 50 simu
 roots, i.e. 38,400 root-simulations per step per GPU.
 
 Per search the device executes exactly what mazero_amd.mcts_sampled runs around the network:
-  k_prepare (RNG stream + root expansion)  ->  selection of simulation 0
-  49 x k_step<expand+backup, select, gather>  ->  k_step<expand+backup>  ->  k_readback
+  k_prepare (RNG stream + root expansion + the selection of simulation 0)
+  49 x fused <expand+backup, select, gather>  ->  1 x <expand+backup>  ->  one k_readback
+where the fused kernel is k_chain (K = 1), k_tree (2 <= K <= 64, pools <= 1024 nodes) or k_step
+(fused_kernel_name below)
 with the network replaced by synthetic device-resident outputs (softmax(N(0,1))
 policy = beta, reward 0.1*N(0,1), value N(0,1), Dirichlet(0.3) root noise, hidden-state pool
 [51, 256, 3*128] fp32 that the fused kernel gathers from).  The whole step (3 searches) is
@@ -23,7 +25,7 @@ anything touches the GPU) and n_gpus is the job's world size.  Roots are indepen
 `--strong` swaps the two.  The barrier / max-over-ranks clock uses torch.distributed (RCCL).
 
 Also reported (rank 0, N=1 only):
-  roofline      dominant kernel k_step<true,true> (fused simulation step): algorithmic bytes per
+  roofline      dominant kernel = the fused simulation step (49 of 52 launches): algorithmic bytes per
                 launch (SURVEY §8d formula over the kernel's own counters) / its average duration,
                 measured with HIP events on the launch stream around a graph of one search's 49
                 back-to-back fused launches; traffic = rocprofv3 FETCH_SIZE+WRITE_SIZE per launch
