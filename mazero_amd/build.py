@@ -63,7 +63,8 @@ def build(force: bool = False, verbose: bool = True, stamps: bool = False) -> st
         return lib
     os.makedirs(OUT_DIR, exist_ok=True)
     tmp = lib + ".tmp"
-    extra = ["-DMZ_STAMPS=1"] if stamps else []
+    # MZ_STAMPS_LEVEL=2: wave 1's node updates in detail instead of the expansion's phases (k_tree)
+    extra = ["-DMZ_STAMPS=" + os.environ.get("MZ_STAMPS_LEVEL", "1")] if stamps else []
     cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), *SRCS, "-o", tmp]
     if verbose:
         print("[mazero_amd] " + " ".join(cmd), flush=True)

@@ -360,6 +360,18 @@ __device__ __forceinline__ int wave_sum(int v) {
     return rl(v, 0) + rl(v, 16) + rl(v, 32) + rl(v, 48);
 }
 
+// Inclusive prefix sum over the wave: row scans by DPP shifts, then the row totals by row
+// broadcasts (all lanes active).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+    return v;
+}
+
 __device__ __forceinline__ bool tame_val(float x) { return x >= -1e30f && x <= 1e30f; }  // false for NaN
 __device__ __forceinline__ bool tame_prior(float x) { return x >= 0.f && x <= 1e30f; }
 
@@ -1007,7 +1019,7 @@ __device__ __forceinline__ void boot_dpp(float &b, float &tmp, float dv, float r
 // --------------------------------------------------------------------------------------------
 template <bool kAsmDma = false>
 __device__ __forceinline__ int stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n, int &nv, int &need,
-                             int &off) {
+                             int &off, unsigned long long *sp = nullptr) {
     const int l = lane_id();
     const int i = i0 + l;
     n = 0;
@@ -1027,6 +1039,10 @@ __device__ __forceinline__ int stage_regions(const Geo &g, const Dev &d, Lds &s,
             need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
         }
     }
+    if (MZ_STAMPS && sp) {
+        asm volatile("" ::"v"(need));
+        sp[0] = __builtin_amdgcn_s_memtime();
+    }
     const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
     // prefix sum of the needed entry counts over the chunk: a uniform loop over the needing lanes
     // only (none in K=1 chains); the chunk ends before the first node that would overflow reg_cap
@@ -1040,6 +1056,10 @@ __device__ __forceinline__ int stage_regions(const Geo &g, const Dev &d, Lds &s,
         }
         if (l == j) off = acc;
         acc += vj;
+    }
+    if (MZ_STAMPS && sp) {
+        asm volatile("" ::"v"(off));
+        sp[1] = __builtin_amdgcn_s_memtime();
     }
     const int2 *gV = d.V() + (size_t)t * g.P * g.E;
     int *regdw = (int *)s.reg;
@@ -2134,6 +2154,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
                 stl[MZ_S_CYC_W1_BACKUP] += (long long)(ts[5] - ts[4]);
                 stl[MZ_S_CYC_W1_SYNC] += (long long)(ts[5] - ts[0]);  // wave 1's whole span
             }
+            for (unsigned long long m = ballot(err != 0); m; m &= m - 1ull) err |= rl(err, __builtin_ctzll(m));  // any lane's
             if (l == 0) {
 #pragma unroll
                 for (int k = 0; k < kStatN; ++k) xst[MZ_S_COUNT + k] = stl[k];  // wave 1's counters
@@ -2872,8 +2893,7 @@ struct TreeLayout {
     static constexpr int oFl = oPS + r16(4 * NC);                  // i32 [NC] 1 + path level (path nodes), else 0
     static constexpr int oAz = oFl + r16(4 * NC);                  // float2 [NC] path nodes' new {value, reward}
     static constexpr int oPath = oAz + r16(8 * NC);                // int2 [PSx] the path {node, visits at selection}
-    static constexpr int oCw = oPath + r16(8 * (PSx + kWave));     // float4 [PSx] path nodes' value-set scalars
-    static constexpr int oLp = oCw + r16(16 * (PSx + kWave));      // f32 lambda powers
+    static constexpr int oLp = oPath + r16(8 * (PSx + kWave));     // f32 lambda powers
     static constexpr int oRng = oLp + r16(4 * (PSx + 1 + kWave));  // u32 [kRngWin] engine words
     static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 bootstrap values
     static constexpr int oReg = oBoot + r16(4 * (PSx + kWave));    // int2 [kRegCap] value entries; big leaf rows
@@ -2885,7 +2905,10 @@ struct TreeLayout {
     static constexpr int oPol = oIx + r16(4 * kWave);              // f32 [64] the leaf's policy
     static constexpr int oNxt = oPol + r16(4 * kWave);             // u32 [64] the header's engine words
     static constexpr int oSt = oNxt + r16(4 * kWave);              // i64 [64] the tree's statistics counters
-    static constexpr int total = oSt + r16(8 * kWave);
+    static constexpr int oCn = oSt + r16(8 * kWave);               // float4 [NC] staged value-set scalars
+    static constexpr int oPb = oCn + r16(16 * NC);                 // f32 [PSx] logf((n + c2 + 1)/c2) + c1
+    static constexpr int oSq = oPb + r16(4 * (PSx + kWave));       // f64 [PSx] sqrt(n)
+    static constexpr int total = oSq + r16(8 * (PSx + kWave));
 };
 int tree_lds_bytes(int nc) {
     switch (nc) {
@@ -2898,14 +2921,79 @@ int tree_lds_bytes(int nc) {
     }
 }
 
+// k_tree, wave 1: stage_regions with every lane's staging offset (exclusive prefix sum of the
+// needed entry counts, by DPP when the chunk fits reg_cap) and the chunk's entry count acc.
+__device__ __forceinline__ int tree_stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n,
+                                                  int &nv, int &need, int &off, int &acc) {
+    const int l = lane_id();
+    const int i = i0 + l;
+    n = 0;
+    nv = 0;
+    need = 0;
+    if (i <= D) {
+        const int2 pe = s.path[i];
+        n = pe.x;
+        nv = pe.y;
+        need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
+    }
+    const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
+    const int nvs = (l < lim && need) ? nv : 0;
+    const int inc = wave_incl_scan(nvs);
+    const int all = rl(inc, 63);
+    int cnt = lim;
+    if (all <= g.reg_cap) {
+        off = inc - nvs;
+        acc = all;
+    } else {  // (rare) the chunk ends before the first node that would overflow reg_cap
+        int a = 0;
+        off = 0;
+        for (unsigned long long m = ballot(nvs > 0); m; m &= m - 1ull) {
+            const int j = __builtin_ctzll(m);
+            const int vj = rl(nv, j);
+            if (a + vj > g.reg_cap) {
+                cnt = j;
+                break;
+            }
+            if (l >= j) off = a + vj;
+            a += vj;
+        }
+        off -= (l < cnt) ? nvs : 0;
+        if (l >= cnt) {
+            need = 0;
+            off = a;
+        }
+        acc = a;
+    }
+    const int2 *gV = d.V() + (size_t)t * g.P * g.E;
+    int *regdw = (int *)s.reg;
+    for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
+        const int j = __builtin_ctzll(m);
+        const int nj = rl(n, j), dw = 2 * rl(nv, j), oj = rl(off, j);
+        const int *src = (const int *)(gV + (size_t)nj * g.E);
+        for (int c = 0; c < dw; c += kWave)
+            if (c + l < dw) glds4a(src + c + l, regdw + 2 * oj + c);
+    }
+    return cnt;
+}
+
+// bits [a, b) of a 64-bit lane mask, clipped to [0, 64)
+__device__ __forceinline__ unsigned long long lane_range(int a, int b) {
+    a = a < 0 ? 0 : a;
+    b = b > kWave ? kWave : b;
+    if (b <= a) return 0ull;
+    const unsigned long long w = (b - a == kWave) ? ~0ull : ((1ull << (b - a)) - 1ull);
+    return w << a;
+}
+
 // CTree::back_propagate (cnode.cpp:415-450) for k_tree: backup()'s arithmetic and value-entry
 // updates, but the staged node records stay as they were (the prior-score waves read them): the
 // path nodes' new {value, reward} go to sAz, their q values into this wave's min / max, the rest to
-// HBM.  Path level i's value-set scalars are sCw[i].
-__device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, const float4 *sCw, float2 *sAz, int t,
+// HBM.  Node n's value-set scalars are sCn[n] (staged with the node records).
+template <bool FLAT>
+__device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, float2 *sAz, int t,
                                             int D, float value, float reward, float disc, int cnt0, int n0, int nv0,
-                                            int need0, int off0, int &err, long long &ent_r, long long &ent_w,
-                                            float &pmn, float &pmx, unsigned long long *tb) {
+                                            int need0, int off0, int acc0, int &err, long long &ent_r, long long &ent_w,
+                                            float &pmn, float &pmx, unsigned long long *tb, const float4 *sCn) {
     const int l = lane_id();
     {  // bootstrap values b_{i-1} = reward_i + discount * b_i (cnode.cpp:424,448), as backup()
         float carry = value;
@@ -2930,7 +3018,8 @@ __device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, 
         stamp(tb, 1);
     }
     int2 *gV = d.V() + (size_t)t * g.P * g.E;
-    int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0;
+    int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0, acc = acc0;
+    (void)acc;
     pmn = INFINITY;
     pmx = -INFINITY;
     for (int i0 = 0; i0 <= D;) {
@@ -2942,32 +3031,65 @@ __device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, 
         wait_lds();
         if (MZ_STAMPS && i0 == 0) stamp(tb, 2);
         const int i = i0 + l;
-        int lo = nv, c = 0, pv = 0;  // entries of a smaller depth / the same depth / same depth, smaller value
         const float key = (l < cnt) ? s.boot[i] : 0.f;
-        for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
-            const int j = __builtin_ctzll(m);
-            const int nvj = rl(nv, j), offj = rl(off, j), depj = D - (i0 + j);
-            const float keyj = rlf(key, j);
-            int cl = 0, cc = 0, cp = 0;
-            for (int e0 = 0; e0 < nvj; e0 += kWave) {
-                const bool on = e0 + l < nvj;
-                const int2 e = on ? s.reg[offj + e0 + l] : make_int2(0x7fffffff, 0);
-                cl += __popcll(ballot(on && e.x < depj));
-                cc += __popcll(ballot(on && e.x == depj));
-                cp += __popcll(ballot(on && e.x == depj && i2f(e.y) < keyj));
+        int lo = 0, c = 0, pv = 0;  // entries of a smaller depth / the same depth / same depth, smaller value
+        if constexpr (FLAT) {
+            // one lane-parallel pass over the chunk's staged entries: lane e holds entry e and
+            // compares it with its owner node's depth class and key; lane j counts over its own
+            // node's range
+            const unsigned long long own = ballot(l < cnt && need && nv > 0);
+            const int nvs = (l < cnt && need) ? nv : 0;
+            for (int e0 = 0; e0 < acc; e0 += kWave) {
+                const int e = e0 + l;
+                const bool on = e < acc;
+                const int2 en = on ? s.reg[e] : make_int2(0x7fffffff, 0);
+                int od = -1;
+                float ok = 0.f;
+                for (unsigned long long m = own; m; m &= m - 1ull) {
+                    const int j = __builtin_ctzll(m);
+                    if (e >= rl(off, j)) {
+                        od = D - (i0 + j);
+                        ok = rlf(key, j);
+                    }
+                }
+                const unsigned long long blt = ballot(on && en.x < od);
+                const unsigned long long beq = ballot(on && en.x == od);
+                const unsigned long long bpv = ballot(on && en.x == od && i2f(en.y) < ok);
+                const unsigned long long wm = lane_range(off - e0, off + nvs - e0);
+                lo += __popcll(blt & wm);
+                c += __popcll(beq & wm);
+                pv += __popcll(bpv & wm);
             }
-            if (l == j) {
-                lo = cl;
-                c = cc;
-                pv = cp;
+            if (!need) lo = nv;
+            ent_r += wave_sum(nvs);
+        } else {
+            lo = nv;
+            for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
+                const int j = __builtin_ctzll(m);
+                const int nvj = rl(nv, j), offj = rl(off, j), depj = D - (i0 + j);
+                const float keyj = rlf(key, j);
+                int cl = 0, cc = 0, cp = 0;
+                for (int e0 = 0; e0 < nvj; e0 += kWave) {
+                    const bool on = e0 + l < nvj;
+                    const int2 e = on ? s.reg[offj + e0 + l] : make_int2(0x7fffffff, 0);
+                    cl += __popcll(ballot(on && e.x < depj));
+                    cc += __popcll(ballot(on && e.x == depj));
+                    cp += __popcll(ballot(on && e.x == depj && i2f(e.y) < keyj));
+                }
+                if (l == j) {
+                    lo = cl;
+                    c = cc;
+                    pv = cp;
+                }
+                ent_r += nvj;
             }
-            ent_r += nvj;
         }
+        if (MZ_STAMPS && i0 == 0) stamp(tb, 3);
         int pos = 0;
         if (l < cnt) {
             const int dep = D - i;
             const int2 *R = s.reg + off;
-            const float4 cw = sCw[i];
+            const float4 cw = sCn[n];  // (the staged value-set scalars)
             float ws = cw.x, tw = cw.y;
             const float lp = s.lp[dep];
             const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
@@ -3022,22 +3144,47 @@ __device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, 
                 pmx = fmaxf(pmx, q);
             }
         }
-        for (unsigned long long m = ballot(l < cnt && nv > pos); m; m &= m - 1ull) {  // tails up by one
-            const int j = __builtin_ctzll(m);
-            const int nvj = rl(nv, j), posj = rl(pos, j), offj = rl(off, j), nj = rl(n, j);
-            ent_w += nvj - posj;
-            int2 *Gj = gV + (size_t)nj * g.E;
-            for (int e0 = posj; e0 < nvj; e0 += kWave)
-                if (e0 + l < nvj) Gj[e0 + l + 1] = s.reg[offj + e0 + l];
+        if (MZ_STAMPS && i0 == 0) stamp(tb, 4);
+        if constexpr (FLAT) {  // the entries at or after each insertion point move up by one, lane-parallel
+            const unsigned long long own = ballot(l < cnt && need && nv > 0);
+            ent_w += wave_sum((l < cnt) ? nv - pos : 0);
+            for (int e0 = 0; e0 < acc; e0 += kWave) {
+                const int e = e0 + l;
+                const int2 en = s.reg[e < acc ? e : 0];
+                int q = -1, pj = 0, nj = 0;
+                for (unsigned long long m = own; m; m &= m - 1ull) {
+                    const int j = __builtin_ctzll(m);
+                    const int oj = rl(off, j);
+                    if (e >= oj) {
+                        q = e - oj;
+                        pj = rl(pos, j);
+                        nj = rl(n, j);
+                    }
+                }
+                if (e < acc && q >= pj) gV[(size_t)nj * g.E + q + 1] = en;
+            }
+        } else {
+            for (unsigned long long m = ballot(l < cnt && nv > pos); m; m &= m - 1ull) {  // tails up by one
+                const int j = __builtin_ctzll(m);
+                const int nvj = rl(nv, j), posj = rl(pos, j), offj = rl(off, j), nj = rl(n, j);
+                ent_w += nvj - posj;
+                int2 *Gj = gV + (size_t)nj * g.E;
+                for (int e0 = posj; e0 < nvj; e0 += kWave)
+                    if (e0 + l < nvj) Gj[e0 + l + 1] = s.reg[offj + e0 + l];
+            }
         }
+        if (MZ_STAMPS && i0 == 0) stamp(tb, 5);
         ent_w += cnt;
         wait_lds();
         i0 += cnt;
-        if (i0 <= D) cnt = stage_regions<true>(g, d, s, t, D, i0, n, nv, need, off);
+        if (i0 <= D) {
+            if constexpr (FLAT) cnt = tree_stage_regions(g, d, s, t, D, i0, n, nv, need, off, acc);
+            else cnt = stage_regions<true>(g, d, s, t, D, i0, n, nv, need, off);
+        }
     }
     if (MZ_STAMPS) {
         wait_lds();
-        stamp(tb, 3);
+        stamp(tb, 6);
     }
 }
 
@@ -3059,6 +3206,13 @@ constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 // 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
 template <int NC>
 constexpr bool kTreeLevels = (NC >= 1024);
+
+// Wave 1's order statistics as one lane-parallel pass over all staged value entries (lane e
+// holds entry e) up to 384-node pools; larger pools count node by node (their long value sets make
+// the per-entry owner search cost more).  k_tree fused launch, same box: 3m K = 5 10.32 ->
+// 10.09 us (with the staged value-set scalars), 3s5z K = 5 11.88 -> 12.11, 27m K = 5 14.13 -> 15.41.
+template <int NC>
+constexpr bool kTreeFlat = (NC <= 384);
 
 template <int NC>
 __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
@@ -3179,7 +3333,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
     int *sFl = (int *)(smem + L::oFl);
     float2 *sAz = (float2 *)(smem + L::oAz);
     int2 *sPath = (int2 *)(smem + L::oPath);
-    float4 *sCw = (float4 *)(smem + L::oCw);
+    float *spb = (float *)(smem + L::oPb);
+    double *ssq = (double *)(smem + L::oSq);
     float *sLp = (float *)(smem + L::oLp);
     unsigned *sRng = (unsigned *)(smem + L::oRng);
     float *xf = (float *)(smem + L::oX);
@@ -3202,12 +3357,25 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 if (wv == 2) {
                     glds16a(d.A() + nb + i0 + l, sA + i0);
                     glds16a(d.Bn() + nb + i0 + l, sB + i0);
+                    glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);
                 } else {
                     glds4a(d.PP() + nb + i0 + l, sPP + i0);
                     glds4a(d.Q() + nb + i0 + l, sQ + i0);
                     glds4a(d.Par() + nb + i0 + l, sPar + i0);
                 }
             }
+#ifdef MZ_ABL_LINES  // experiment: MZ_ABL_LINES x 16 extra cache lines in round 1 (value entries, discarded)
+        if (wv == 2) {
+            const int2 *gVt = (const int2 *)(d.base + (size_t)pl->d.o_V * 256) + (size_t)t * P * pl->g.E;
+            for (int k = 0; k < MZ_ABL_LINES; ++k) glds16a((const char *)gVt + 1024 * k + 16 * l, smem + L::oReg + 1024 * k);
+        }
+#endif
+        if (SEL && !kTreeLevels<NC> && wv == 3) {  // the pUCT factors per parent visit count (no gathers)
+            for (int i0 = 0; i0 < PS; i0 += kWave)
+                if (i0 + l < PS) glds4a(d.pb() + i0 + l, spb + i0);
+            for (int i0 = 0; i0 < 2 * PS; i0 += kWave)
+                if (i0 + l < 2 * PS) glds4a((const int *)d.sq() + i0 + l, (int *)ssq + i0);
+        }
         const int herr = hp0->err, tot = hp0->tot;
         if (herr) {
             wait_vm();
@@ -3219,6 +3387,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                     if (wv == 2) {
                         glds16a(d.A() + nb + i0 + l, sA + i0);
                         glds16a(d.Bn() + nb + i0 + l, sB + i0);
+                        glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);
                     } else {
                         glds4a(d.PP() + nb + i0 + l, sPP + i0);
                         glds4a(d.Q() + nb + i0 + l, sQ + i0);
@@ -3230,6 +3399,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         // nodes 1 .. tot-1 in 64-node blocks, alternating between the two waves
         constexpr int NBW = (NC + 2 * kWave - 1) / (2 * kWave);
         const float *T = d.T();
+        (void)T;
         float pbc[NBW];
         float mn = INFINITY, mx = -INFINITY;
         int cv = 0;
@@ -3244,8 +3414,12 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 const int fn = sFl[n];
                 int v = a.x + (fn ? 1 : 0);
                 if (SEL && np >= 0 && np < PS) {
-                    if (v > np) v = np;  // (not in a consistent tree; keeps the read in range)
-                    pbc[k] = T[np * (np + 1) / 2 + v];
+                    if (v > np) v = np;  // (not in a consistent tree; as the host table's range)
+                    // pb_c (cnode.cpp:313-314): the host-built table for the 1024-node class (its many
+                    // nodes make the double division cost more than the gathers), else from the
+                    // staged per-n factors with the same double arithmetic
+                    if constexpr (kTreeLevels<NC>) pbc[k] = T[np * (np + 1) / 2 + v];
+                    else pbc[k] = (float)((double)spb[np] * (ssq[np] / (double)(v + 1)));
                 }
                 if (a.x > 0 && !fn) {
                     const float q = sQ[n];
@@ -3316,11 +3490,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         stamp(ts, 1);
         // the path nodes' value-set scalars, then the value entries the updates need
         // (stage_regions), the bootstrap chain meanwhile
-        for (int i0 = 0; i0 <= D; i0 += kWave)
-            if (i0 + l <= D) {
-                const int n = sPath[i0 + l].x;
-                glds16a(d.C() + nb + ((n >= 0 && n < tot) ? n : 0), sCw + i0);
-            }
         Lds s{};
         s.A = sA;
         s.B = sB;
@@ -3331,15 +3500,21 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
         s.reg = (int2 *)(smem + L::oReg);
         int n0 = 0, nv0 = 0, need0 = 0, off0 = 0;
         int err = 0;
-        const int cnt0 = stage_regions<true>(g, d, s, t, D, 0, n0, nv0, need0, off0);
+        unsigned long long tsr[3] = {0};
+        stamp(tsr, 2);
+        int acc0 = 0;
+        int cnt0;
+        if constexpr (kTreeFlat<NC>) cnt0 = tree_stage_regions(g, d, s, t, D, 0, n0, nv0, need0, off0, acc0);
+        else cnt0 = stage_regions<true>(g, d, s, t, D, 0, n0, nv0, need0, off0, tsr);
         long long ent_r = 0, ent_w = 0;
         float pmn, pmx;
-        unsigned long long tb[5] = {0};
+        unsigned long long tb[8] = {0};
         stamp(tb, 0);
-        backup_tree(g, d, s, sCw, sAz, t, D, v_in, r_in, discount, cnt0, n0, nv0, need0, off0, err, ent_r, ent_w, pmn,
-                    pmx, tb);
+        backup_tree<kTreeFlat<NC>>(g, d, s, sAz, t, D, v_in, r_in, discount, cnt0, n0, nv0, need0, off0, acc0, err, ent_r, ent_w,
+                    pmn, pmx, tb, (const float4 *)(smem + L::oCn));
         pmn = wave_min_to63(pmn);
         pmx = wave_max_to63(pmx);
+        for (unsigned long long m = ballot(err != 0); m; m &= m - 1ull) err |= rl(err, __builtin_ctzll(m));  // any lane's
         if (l == 63) {
             xf[0] = pmn;
             xf[1] = pmx;
@@ -3353,7 +3528,17 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
                 xl[3] = (long long)(tb[0] - ts[1]);
                 xl[4] = (long long)(tb[1] - tb[0]);
                 xl[5] = (long long)(tb[2] - tb[1]);
-                xl[6] = (long long)(tb[3] - tb[2]);
+                xl[6] = (long long)(tb[6] - tb[2]);
+#if MZ_STAMPS >= 3  // wave 1's staging in detail
+                xl[7] = (long long)(tsr[2] - ts[1]);  // value-set scalars issued
+                xl[8] = (long long)(tsr[0] - tsr[2]);  // path records and need flags read
+                xl[9] = (long long)(tsr[1] - tsr[0]);  // staging offsets
+                xl[10] = (long long)(tb[0] - tsr[1]);  // value entries issued
+#else
+                xl[7] = (long long)(tb[3] - tb[2]);  // first chunk: entry counts
+                xl[8] = (long long)(tb[4] - tb[3]);  // node updates and stores
+                xl[9] = (long long)(tb[5] - tb[4]);  // tail shifts
+#endif
             }
         }
         lds_barrier();  // (2): its global stores stay in flight
@@ -3838,16 +4023,28 @@ __global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA,
             case MZ_S_CYC_W1_SYNC: add = (long long)(tp[1] - tp[0]); break;   // (barrier + tie lists)
             case MZ_S_CYC_SELECT: add = (long long)(tp[3] - ts[5]); break;    // the chase
             case MZ_S_CYC_BAK_WAIT: add = (long long)(ts[6] - tp[3]); break;  // path record + outputs
+#if MZ_STAMPS < 3
             case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;
+#endif
             case MZ_S_CYC_EPILOGUE: add = (long long)(ts[8] - ts[7]); break;
             case MZ_S_STAMPED: add = 1; break;
             case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1 after barrier (1)
+#if MZ_STAMPS >= 2  // wave 1's node updates in detail, in place of the expansion's phases
+            case MZ_S_CYC_EXP_CDF: add = xl[7]; break;    // entry counts (first chunk)
+            case MZ_S_CYC_EXP_DRAW: add = xl[8]; break;   // node updates and stores
+            case MZ_S_CYC_EXP_NODES: add = xl[9]; break;  // tail shifts
+#if MZ_STAMPS >= 3
+            case MZ_S_CYC_GATHER: add = xl[10]; break;
+#endif
+#else
             case MZ_S_CYC_EXP_CDF: add = (long long)(tq[0] - ts[0]); break;   // round 1 landed
             case MZ_S_CYC_EXP_DRAW: add = (long long)(tq[1] - tq[0]); break;  // sampling distribution
             case MZ_S_CYC_EXP_NODES: add = (long long)(tq[2] - tq[1]); break; // K draws
+#endif
             case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? xl[3] : 0; break;       // wave 1: staging issue
             case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? xl[5] : 0; break;      // wave 1: entries landed
             case MZ_S_CYC_W1_ROUND1: add = MZ_STAMPS ? xl[6] : 0; break;      // wave 1: node updates
+            case MZ_S_CYC_W1_STAGE2: add = MZ_STAMPS ? xl[4] : 0; break;      // wave 1: bootstrap values
             default: break;
         }
         st[l] = st_old + add;

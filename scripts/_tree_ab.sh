@@ -3,8 +3,10 @@
 # the previous kernels (MZ_NO_TREE=1), plus the stamped build.  Every GPU step has its own limit.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/tree_pytest.log 2>&1
-rc=$?; tail -4 gpurun_out/tree_pytest.log; [ $rc -ne 0 ] && exit $rc
+if [ -z "$NO_TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/tree_pytest.log 2>&1
+  rc=$?; tail -4 gpurun_out/tree_pytest.log; [ $rc -ne 0 ] && exit $rc
+fi
 out=gpurun_out/tree_ab.jsonl; : > $out
 CONFIGS=${CONFIGS:-"k1 k5 3s5z 27m5"}
 for c in $CONFIGS; do
@@ -19,6 +21,9 @@ for c in $CONFIGS; do
   timeout -k 10 200 python bench.py --no-cpu $args >> $out 2>> gpurun_out/tree_ab.err || exit $?
   [ -n "$AB" ] && { MZ_NO_TREE=1 timeout -k 10 200 python bench.py --no-cpu $args >> $out 2>> gpurun_out/tree_ab.err || exit $?; }
   [ -n "$STAMPS" ] && { MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu $args >> $out 2>> gpurun_out/tree_ab.err || exit $?; }
+  for v in $VARIANTS; do  # experiment builds: mazero_amd/_build/<name>.so
+    MZ_LIB_OVERRIDE=mazero_amd/_build/$v.so timeout -k 10 200 python bench.py --no-cpu $args >> $out 2>> gpurun_out/tree_ab.err || exit $?
+  done
 done
 python - $out <<'PY'
 import json, sys
