@@ -2487,9 +2487,9 @@ __device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp)
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
-__global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA, int pk, const float *reward,
-                                               const float *value, const float *policy, const float *beta, int K,
-                                               int hsx, float discount, int fast_ok, const char *pool,
+__global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, const float *beta, int P, int PS,
+                                               int BA, int pk, int hsx, int K, float discount, int fast_ok,
+                                               const float *reward, const float *value, const char *pool,
                                                long long pool_stride, long long row_bytes, char *gather_out,
                                                int *idx_x, int *idy, int *act) {
     (void)pk;
@@ -2514,6 +2514,25 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     unsigned long long ts[8] = {0};
     stamp(ts, 0);
     // ---- round 1: everything, from the arguments (the chain's length is hsx) ----
+    // the header, the leaf's structure record and the handle's constants (scalar loads from the
+    // preloaded arena base, issued first; the network outputs follow the LDS-DMA below)
+    TreeHdr h;
+    {
+        const cTreeHdr *hp = (const cTreeHdr *)(d.hdr() + t);
+        h.cursor = hp->cursor;
+        h.tot = hp->tot;
+        h.D = hp->D;
+        h.err = hp->err;
+        h.tame = hp->tame;
+        h.leaf = hp->leaf;
+        h.nxt[0] = hp->nxt[0];
+        h.nxt[1] = hp->nxt[1];
+    }
+    const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
+    const int gW = pl->g.W;
+    const float omr = pl->g.one_minus_rho;
+    const unsigned oR = pl->d.o_R;
+    d.o_D = pl->d.o_D;
     int Dp = hsx;  // back-propagation path 0..Dp, leaf Dp, tot = Dp + 1
     if (Dp < 0 || Dp + 1 > P) Dp = 0;
     float pol = 0.f, bet = 0.f;
@@ -2522,10 +2541,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
     int4 leaf_b = make_int4(0, 0, 0, 0);
     // the next leaf's parent is this launch's leaf (hidden_state_index_x = hsx): its row is
     // fetched now and stored at the end (four 16-byte chunks per lane up to 4 KiB, LDS-DMA above)
-    const bool row_al = SEL && pool && (((row_bytes | pool_stride | (long long)(uintptr_t)pool |
-                                          (long long)(uintptr_t)gather_out) & 15) == 0);
-    const bool g_reg = row_al && row_bytes <= 4 * 16 * kWave;
-    const bool g_lds = row_al && !g_reg && row_bytes <= 16 * 16 * kWave;
+    bool row_al = false, g_reg = false, g_lds = false;
     int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
     // Round 1 is LDS-DMA and scalar loads (invisible to the compiler's wait counting) plus, last,
     // the leaf row's loads: the counted wait below leaves exactly those in flight until the end.
@@ -2545,6 +2561,17 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
         glds4a(beta + ib, sW);  // (lanes >= A: zero weights, below)
         glds4a((const int *)st + (l < 2 * MZ_S_COUNT ? l : 0), (int *)sSt);
         if (l == 0) glds16a(d.Bn() + nb + Dp, smem + L.oLb);
+        // the leaf-row arguments are not preloaded: their kernel-argument load is first waited for
+        // here, after the loads above were issued (the asm keeps the compiler from computing the
+        // row's class, and so waiting, any earlier)
+        unsigned long long pool_u = (unsigned long long)(uintptr_t)pool, out_u = (unsigned long long)(uintptr_t)gather_out;
+        asm volatile("" : "+s"(pool_u), "+s"(pool_stride), "+s"(row_bytes), "+s"(out_u));
+        pool = (const char *)(const gchar *)(uintptr_t)pool_u;
+        gather_out = (char *)(uintptr_t)out_u;
+        row_al = SEL && pool && (((row_bytes | pool_stride | (long long)(uintptr_t)pool |
+                                   (long long)(uintptr_t)gather_out) & 15) == 0);
+        g_reg = row_al && row_bytes <= 4 * 16 * kWave;
+        g_lds = row_al && !g_reg && row_bytes <= 16 * 16 * kWave;
         if (g_reg || g_lds) {
             const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
             const long long last = row_bytes - 16, o = (long long)l * 16;
@@ -2562,25 +2589,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, int P, int PS, int BA
         for (int i0 = 0; i0 <= Dp; i0 += kWave)
             if (i0 + l <= Dp) glds4a(&d.A()[nb + i0 + l].w, sR + i0);
     }
-    // the header, the leaf's structure record and the network outputs of this tree (scalar loads)
-    TreeHdr h;
-    {
-        const cTreeHdr *hp = (const cTreeHdr *)(d.hdr() + t);
-        h.cursor = hp->cursor;
-        h.tot = hp->tot;
-        h.D = hp->D;
-        h.err = hp->err;
-        h.tame = hp->tame;
-        h.leaf = hp->leaf;
-        h.nxt[0] = hp->nxt[0];
-        h.nxt[1] = hp->nxt[1];
-    }
     const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
-    const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
-    const int gW = pl->g.W;
-    const float omr = pl->g.one_minus_rho;
-    const unsigned oR = pl->d.o_R;
-    d.o_D = pl->d.o_D;
     if (wv == 0 && g_reg) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");        // the row stays in flight
     else if (wv == 0 && g_lds) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // (its chunks too)
     else wait_vm();
@@ -3307,9 +3316,9 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
-__global__ __launch_bounds__(256) void k_tree(char *base, int P, int PS, int BA, int pk, const float *reward,
-                                              const float *value, const float *policy, const float *beta, int K,
-                                              int hsx, float discount, int fast_ok, const char *pool,
+__global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, const float *beta, int P, int PS,
+                                              int BA, int pk, int hsx, int K, float discount, int fast_ok,
+                                              const float *reward, const float *value, const char *pool,
                                               long long pool_stride, long long row_bytes, char *gather_out,
                                               int *idx_x, int *idy, int *act) {
     // Each wave role runs to its own return: no control-flow join follows the split, so the
@@ -4346,18 +4355,19 @@ void set_lds_limit(int lds) {
 template <int NC, bool SEL = true>
 void launch_chain(mz_batch *b, const StepArgs &a, int lds) {
     const Geo &g = b->geo;
-    hipLaunchKernelGGL((k_chain<NC, SEL>), dim3(g.B), dim3(2 * kWave), lds, b->stream, (char *)b->dev.base, g.P, g.PS,
-                       g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value, a.policy, a.beta, a.K, a.hsx,
-                       a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy,
-                       a.act);
+    // (the first 14 argument dwords, through the discount, arrive preloaded in SGPRs: round 1 needs no
+    // kernel-argument load)
+    hipLaunchKernelGGL((k_chain<NC, SEL>), dim3(g.B), dim3(2 * kWave), lds, b->stream, (char *)b->dev.base, a.policy,
+                       a.beta, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.hsx, a.K, a.discount, b->fast_ok,
+                       a.reward, a.value, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act);
 }
 
 template <int NC, bool SEL = true>
 void launch_tree(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
     hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(4 * kWave), TreeLayout<NC>::total, b->stream,
-                       (char *)b->dev.base, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.reward, a.value,
-                       a.policy, a.beta, a.K, a.hsx, a.discount, b->fast_ok, a.pool, a.pool_stride, a.row_bytes,
+                       (char *)b->dev.base, a.policy, a.beta, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.hsx,
+                       a.K, a.discount, b->fast_ok, a.reward, a.value, a.pool, a.pool_stride, a.row_bytes,
                        a.gather_out, a.idx_x, a.idy, a.act);
 }
 
