@@ -2528,6 +2528,8 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
         h.nxt[0] = hp->nxt[0];
         h.nxt[1] = hp->nxt[1];
     }
+    // the root's visit count before this back-propagation (wave 0's selection; wave 1 owns sA)
+    const int root_vis0 = *(const __attribute__((address_space(4))) int *)&d.A()[nb].x;
     const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
     const int gW = pl->g.W;
     const float omr = pl->g.one_minus_rho;
@@ -2549,13 +2551,6 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
     float *sW = (float *)(smem + L.oW);
     long long *sSt = (long long *)(smem + L.oSt);
     if (wv == 0) {
-        for (int i0 = 0; i0 <= Dp; i0 += kWave)
-            if (i0 + l <= Dp) {
-                glds16a(d.A() + nb + i0 + l, sA + i0);
-                glds16a(d.C() + nb + i0 + l, sC + i0);
-                glds4a(d.PP() + nb + i0 + l, sPP + i0);
-                glds4a(d.lp() + i0 + l, sLp + i0);
-            }
         const size_t ib = (size_t)t * A + (l < A ? l : 0);
         glds4a(policy + ib, sPol);
         glds4a(beta + ib, sW);  // (lanes >= A: zero weights, below)
@@ -2585,9 +2580,14 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
                 for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
             }
         }
-    } else {
+    } else {  // wave 1 back-propagates: the chain's node records
         for (int i0 = 0; i0 <= Dp; i0 += kWave)
-            if (i0 + l <= Dp) glds4a(&d.A()[nb + i0 + l].w, sR + i0);
+            if (i0 + l <= Dp) {
+                glds16a(d.A() + nb + i0 + l, sA + i0);
+                glds16a(d.C() + nb + i0 + l, sC + i0);
+                glds4a(d.PP() + nb + i0 + l, sPP + i0);
+                glds4a(d.lp() + i0 + l, sLp + i0);
+            }
     }
     const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
     if (wv == 0 && g_reg) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");        // the row stays in flight
@@ -2632,17 +2632,14 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
             wait_vm();
             return;
         }
-        for (int i0 = 0; i0 <= D; i0 += kWave)
-            if (i0 + l <= D) {
-                if (wv == 0) {
+        if (wv == 1)
+            for (int i0 = 0; i0 <= D; i0 += kWave)
+                if (i0 + l <= D) {
                     glds16a(d.A() + nb + i0 + l, sA + i0);
                     glds16a(d.C() + nb + i0 + l, sC + i0);
                     glds4a(d.PP() + nb + i0 + l, sPP + i0);
                     glds4a(d.lp() + i0 + l, sLp + i0);
-                } else {
-                    glds4a(&d.A()[nb + i0 + l].w, sR + i0);
                 }
-            }
         if (wv == 0 && l == 0) glds16a(d.Bn() + nb + D, smem + L.oLb);
         wait_vm();
         if (wv == 0) leaf_b = *(const int4 *)(smem + L.oLb);
@@ -2658,7 +2655,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
             const int nl = hi - lo;
             const int lev = hi - 63 + l;
             float rn = 0.f;  // reward of the level above this lane's
-            if (lev >= lo && lev < hi) rn = (lev + 1 == D) ? r_in : sR[lev + 1];
+            if (lev >= lo && lev < hi) rn = (lev + 1 == D) ? r_in : i2f(sA[lev + 1].w);
             float b = (l == 63) ? carry : 0.f;
             float tmp = (l == 62) ? dv * carry : 0.f;
             boot_dpp(b, tmp, dv, rn, nl);
@@ -2667,12 +2664,47 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
             carry = rlf(b, 63 - nl);
             hi = lo;
         }
-        if (MZ_STAMPS) {
-            wait_lds();
-            stamp(ts, 2);
-            if (l == 0) *(unsigned long long *)(smem + L.oR) = ts[2] - ts[1];  // (wave 1: the chain; sR[0..1] are free now)
+        wait_lds();
+        stamp(ts, 2);
+        // ---- CTree::back_propagate (cnode.cpp:415-450) over the chain, lane i = node i ----
+        float mn = INFINITY, mx = -INFINITY;
+        for (int i0 = 0; i0 <= D; i0 += kWave) {
+            const int i = i0 + l;
+            if (i <= D) {
+                const int dep = D - i;
+                const float key = sBoot[i];
+                int4 a4 = sA[i];
+                if (i == D) a4.w = f2i(r_in);  // the leaf's reward is this simulation's
+                const float4 cw = sC[i];
+                const float lp = sLp[dep];
+                float ws = cw.x, tw = cw.y;
+                tw += lp;  // an empty depth class: big gets the value (utils.cpp:36-44)
+                ws += lp * key;
+                const float val = ws / tw;  // CNode::value (cnode.cpp:42-56); every chain node has a child
+                const int4 na = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
+                sA[i] = na;
+                d.A()[nb + i] = na;
+                *(float2 *)&d.C()[nb + i] = make_float2(ws, tw);
+                if (i >= 1) {
+                    const float q = (i2f(a4.w) + discount * val) - sPP[i];  // get_qsa - father->pred_value
+                    mn = fminf(mn, q);
+                    mx = fmaxf(mx, q);
+                }
+            }
+        }
+        // min / max over the q of the visited non-root nodes: the whole chain 1..D
+        mn = unif(rlf(wave_min_to63(mn), 63));
+        mx = unif(rlf(wave_max_to63(mx), 63));
+        if (l == 0) {
+            sR[2] = mn;
+            sR[3] = mx;
+            if (MZ_STAMPS) {
+                *(unsigned long long *)(smem + L.oR) = ts[2] - ts[1];  // the bootstrap chain
+                *(unsigned long long *)(smem + L.oR + 16) = __builtin_amdgcn_s_memtime() - ts[2];  // node updates
+            }
         }
         lds_barrier();
+        wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
     }
 
@@ -2714,7 +2746,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
     const int Ds = c;
     int root_visit = 0, words = 0;
     if (SEL && fast) {
-        root_visit = uni(sA[0].x) + 1;
+        root_visit = root_vis0 + 1;
         if (root_visit - 1 >= PS) err |= kErrTable;
         words = Ds - ((root_visit <= 1) ? 1 : 0);
     }
@@ -2725,38 +2757,10 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
     if (fast && l < kNxt && cursor + words + l < gW) nxt_w = Rt[cursor + words + l];
     if (value_lim(1, omr) != 1) err |= kErrValueSet;  // (count 1: size_lim must be 1, utils.cpp:31)
 
-    // ---- CTree::back_propagate (cnode.cpp:415-450) over the chain, lane i = node i ----
     stamp(ts, 3);
-    lds_barrier();  // the bootstrap values
+    lds_barrier();  // wave 1's back-propagation (sA, sPP updated) and min / max
     stamp(ts, 4);
-    float mn = INFINITY, mx = -INFINITY;
-    for (int i0 = 0; i0 <= D; i0 += kWave) {
-        const int i = i0 + l;
-        if (i <= D) {
-            const int dep = D - i;
-            const float key = sBoot[i];
-            int4 a4 = sA[i];
-            if (i == D) a4.w = f2i(r_in);  // the leaf's reward is this simulation's
-            const float4 cw = sC[i];
-            const float lp = sLp[dep];
-            float ws = cw.x, tw = cw.y;
-            tw += lp;  // an empty depth class: big gets the value (utils.cpp:36-44)
-            ws += lp * key;
-            const float val = ws / tw;  // CNode::value (cnode.cpp:42-56); every chain node has a child
-            const int4 na = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
-            sA[i] = na;
-            d.A()[nb + i] = na;
-            *(float2 *)&d.C()[nb + i] = make_float2(ws, tw);
-            if (i >= 1) {
-                const float q = (i2f(a4.w) + discount * val) - sPP[i];  // get_qsa - father->pred_value
-                mn = fminf(mn, q);
-                mx = fmaxf(mx, q);
-            }
-        }
-    }
-    // min / max over the q of the visited non-root nodes: the whole chain 1..D
-    mn = unif(rlf(wave_min_to63(mn), 63));
-    mx = unif(rlf(wave_max_to63(mx), 63));
+    float mn = unif(sR[2]), mx = unif(sR[3]);  // wave 1's min / max over the q of nodes 1..D
     stamp(ts, 5);
     const int mm_cnt = D;
 
@@ -2850,7 +2854,8 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
             case MZ_S_CYC_EXP_CDF: add = (long long)(ts[2] - ts[1]); break;  // distribution + draw
             case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;   // child, header words
             case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;   // wait for the chain
-            case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;   // node updates + min/max
+            case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;   // min / max read
+            case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? *(const long long *)(smem + L.oR + 16) : 0; break;  // wave 1
             case MZ_S_CYC_SELECT: add = (long long)(ts[6] - ts[5]); break;   // selection
             case MZ_S_CYC_EPILOGUE: add = (long long)(ts[7] - ts[6]); break; // outputs, header
             case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? *(const long long *)(smem + L.oR) : 0; break;
