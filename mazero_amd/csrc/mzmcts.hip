@@ -2442,6 +2442,28 @@ __device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double 
     return cp;
 }
 
+// n dwords global -> LDS by LDS-DMA (asm, uncounted by the compiler): 16-byte chunks when src and dst
+// are 16-byte aligned (a quarter of the instructions; up to 3 dwords past n are read and written:
+// callers' arrays are padded), else dwords
+__device__ __forceinline__ void dma_dwords(const void *src, unsigned lds, int n, bool al16) {
+    const int l = lane_id();
+    if (al16) {
+        const int n4 = (n + 3) >> 2;
+        for (int c = 0; c < n4; c += kWave)
+            if (c + l < n4)
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"((const int4 *)src + c + l),
+                             "s"(lds + 16u * c)
+                             : "memory", "m0");
+    } else {
+        for (int c = 0; c < n; c += kWave)
+            if (c + l < n)
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"((const int *)src + c + l),
+                             "s"(lds + 4u * c)
+                             : "memory", "m0");
+    }
+}
+__device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(uintptr_t)(lds_void *)p; }
+
 // A wave-uniform load through the scalar cache (s_load: counted by lgkmcnt, not vmcnt)
 __device__ __forceinline__ float ldsc(const float *p) {
     return *(const __attribute__((address_space(4))) float *)p;
@@ -2894,6 +2916,9 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
 // expansion / back-propagation / prior scores.  The engine-word draws of the expansion need no
 // staged record and run before the first.
 // --------------------------------------------------------------------------------------------
+constexpr int kBk = 3;                               // back-propagation waves of k_tree
+constexpr int kBkCap = (kRegCap / (2 * kBk)) & ~1;  // value entries per staging slot (two per wave)
+
 template <int NC>
 struct TreeLayout {
     static constexpr int r16(int x) { return (x + 15) & ~15; }
@@ -2909,8 +2934,8 @@ struct TreeLayout {
     static constexpr int oPath = oAz + r16(8 * NC);                // int2 [PSx] the path {node, visits at selection}
     static constexpr int oLp = oPath + r16(8 * (PSx + kWave));     // f32 lambda powers
     static constexpr int oRng = oLp + r16(4 * (PSx + 1 + kWave));  // u32 [kRngWin] engine words
-    static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 bootstrap values
-    static constexpr int oReg = oBoot + r16(4 * (PSx + kWave));    // int2 [kRegCap] value entries; big leaf rows
+    static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 [kBk][PSx + 64] bootstrap values
+    static constexpr int oReg = oBoot + r16(4 * kBk * (PSx + kWave));  // int2 [kRegCap] value entries; big leaf rows
     static constexpr int oX = oReg + r16(8 * kRegCap);             // exchange between the waves
     static constexpr int oW = oX + r16(256);                       // f32 [64] sampling weights
     static constexpr int oP = oW + r16(4 * kWave);                 // f64 [64] probabilities, then the CDF
@@ -3202,6 +3227,208 @@ __device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_tree's back-propagation on three waves: path level i belongs to wave 1 + i % 3 (kBk waves).
+// A wave stages the value entries of its first two levels before barrier (1), from path records it
+// reads with scalar loads (every entry of the node: stage_regions' need test reads structure records
+// that land only at barrier (1)); a third or later level is staged after the previous one is done.
+// After barrier (1) each wave computes the bootstrap values itself and updates its nodes: one
+// lane-parallel pass over a node's entries for the order statistics (utils.cpp:20-71), the node's
+// scalars on every lane, the tail shift of the sorted entries lane-parallel.
+// ------------------------------------------------------------------------------------------------
+
+struct BkPre {
+    int n0, nv0, n1, nv1;  // the pre-staged levels' nodes and entry counts (nv < 0: not staged)
+    int ndma;              // LDS-DMA instructions issued for them (the wave's last ones before barrier (1))
+};
+
+// s_waitcnt vmcnt(n) for a wave-uniform n: all but the wave's n most recent vector-memory operations
+__device__ __forceinline__ void wait_vm_but(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+__device__ __forceinline__ int2 ldsc2(const int2 *p) {
+    const long long v = *(const __attribute__((address_space(4))) long long *)p;
+    return make_int2((int)(v & 0xffffffffll), (int)(v >> 32));
+}
+
+// the path records of wave k's first two levels (scalar loads, issued at the wave's start: indices
+// clamped into the tree's PS records, so the reads need not wait for the header's path length)
+__device__ __forceinline__ void bk_path_records(const Dev &d, int t, int PS, int k, int2 &p0, int2 &p1) {
+    const int2 *gp = d.path() + (size_t)t * PS;
+    p0 = ldsc2(gp + (k < PS ? k : PS - 1));
+    p1 = ldsc2(gp + (k + kBk < PS ? k + kBk : PS - 1));
+}
+
+// their value entries -> the wave's two staging slots (every entry of the node)
+__device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, int D, int k, int2 p0, int2 p1,
+                                             int2 *sReg) {
+    const int l = lane_id();
+    BkPre r{0, -1, 0, -1, 0};
+    const int2 *gV = d.V() + (size_t)t * P * E;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int i = k + kBk * j;
+        const int2 pe = j == 0 ? p0 : p1;
+        if (i > D) break;
+        if (pe.x < 0 || pe.x >= P || pe.y < 0 || pe.y > kBkCap) continue;  // (staged after barrier (1))
+        const int *src = (const int *)(gV + (size_t)pe.x * E);
+        int *dst = (int *)(sReg + (2 * k + j) * kBkCap);
+        for (int c = 0; c < 2 * pe.y; c += kWave)
+            if (c + l < 2 * pe.y) glds4a(src + c + l, dst + c);
+        r.ndma += (2 * pe.y + kWave - 1) / kWave;
+        if (j == 0) {
+            r.n0 = pe.x;
+            r.nv0 = pe.y;
+        } else {
+            r.n1 = pe.x;
+            r.nv1 = pe.y;
+        }
+    }
+    return r;
+}
+
+// the bootstrap values b_{i-1} = reward_i + discount * b_i (cnode.cpp:424,448) of levels 0..D into boot[]
+__device__ __forceinline__ void bk_boot(const Lds &s, float *boot, int D, float value, float reward, float disc) {
+    const int l = lane_id();
+    float carry = value;
+    int hi = D;
+    while (true) {
+        const int lo = hi > 63 ? hi - 63 : 0;
+        const int nl = hi - lo;
+        const int lev = hi - 63 + l;
+        float rn = 0.f;
+        if (lev >= lo && lev < hi) rn = (lev + 1 == D) ? reward : i2f(s.A[s.path[lev + 1].x].w);
+        float b = (l == 63) ? carry : 0.f;
+        float tmp = (l == 62) ? disc * carry : 0.f;
+        boot_dpp(b, tmp, disc, rn, nl);
+        if (lev >= lo && lev <= hi) boot[lev] = b;
+        if (lo == 0) break;
+        carry = rlf(b, 63 - nl);
+        hi = lo;
+    }
+    wait_lds();
+}
+
+// wave k's path levels k, k + kBk, ... (CTree::back_propagate, cnode.cpp:415-450, node by node)
+__device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds &s, const float4 *sCn, float2 *sAz,
+                                          const float *boot, int2 *sReg, BkPre pre, int t, int D, float reward,
+                                          float disc, int k, int &err, long long &ent_r, long long &ent_w, float &pmn,
+                                          float &pmx) {
+    const int l = lane_id();
+    int2 *gV = d.V() + (size_t)t * g.P * g.E;
+    pmn = INFINITY;
+    pmx = -INFINITY;
+    wait_vm();  // the pre-staged entries (in flight across barrier (1))
+    for (int j = 0, i = k; i <= D; ++j, i += kBk) {
+        const int2 pe = s.path[i];
+        const int n = uni(pe.x), nv = uni(pe.y);
+        if (n < 0 || n >= g.P || nv < 0 || nv > kBkCap) {
+            err |= kErrPath;
+            continue;
+        }
+        const int2 *R;
+        if (j == 0 && pre.nv0 == nv && pre.n0 == n) {
+            R = sReg + (2 * k) * kBkCap;
+        } else if (j == 1 && pre.nv1 == nv && pre.n1 == n) {
+            R = sReg + (2 * k + 1) * kBkCap;
+        } else {  // a later level (or a pre-stage that did not match): slot 0, free once level j - 2 is done
+            int2 *dst = sReg + (2 * k) * kBkCap;
+            const int *src = (const int *)(gV + (size_t)n * g.E);
+            for (int c = 0; c < 2 * nv; c += kWave)
+                if (c + l < 2 * nv) glds4a(src + c + l, (int *)dst + c);
+            wait_vm();
+            R = dst;
+        }
+        const int dep = D - i;
+        const float key = boot[i];
+        const int4 b4 = uni4(s.B[n]);
+        // entries of a smaller depth / the same depth / the same depth and a smaller value; none but
+        // smaller depths when the node's deepest entry is above dep (stage_regions' need test)
+        int lo = nv, c = 0, pv = 0;
+        if (nv > 0 && md_of(b4.y) >= dep) {
+            lo = 0;
+            for (int e0 = 0; e0 < nv; e0 += kWave) {
+                const bool on = e0 + l < nv;
+                const int2 e = on ? R[e0 + l] : make_int2(0x7fffffff, 0);
+                lo += __popcll(ballot(on && e.x < dep));
+                c += __popcll(ballot(on && e.x == dep));
+                pv += __popcll(ballot(on && e.x == dep && i2f(e.y) < key));
+            }
+            ent_r += nv;
+        }
+        const float4 cw = sCn[n];
+        float ws = cw.x, tw = cw.y;
+        const float lp = s.lp[dep];
+        const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
+        const int nl = value_lim(c + 1, g.one_minus_rho);
+        if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
+            const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
+            if (!(key < mb)) {
+                ws -= lp * mb;
+                tw -= lp;
+                tw += lp;
+                ws += lp * key;
+            }
+        } else {
+            if (cur + 1 != nl) err |= kErrValueSet;
+            if (c - cur == 0) {
+                tw += lp;
+                ws += lp * key;
+            } else {
+                const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
+                if (key > ms) {
+                    tw += lp;
+                    ws += lp * key;
+                } else {
+                    tw += lp;
+                    ws += lp * ms;
+                }
+            }
+        }
+        int pos = lo + pv;
+        int2 *G = gV + (size_t)n * g.E;
+        if (nv + 1 > g.E) {
+            err |= kErrPath;
+            pos = nv;
+        } else if (l == 0) {
+            G[pos] = make_int2(dep, f2i(key));
+        }
+        for (int e0 = pos; e0 < nv; e0 += kWave)  // the entries after the insertion point move up by one
+            if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
+        ent_w += nv - pos + 1;
+        const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
+        int4 a4 = uni4(s.A[n]);
+        if (is_leaf) a4.w = f2i(reward);
+        const int nc = is_leaf ? 1 : nc_of(b4.y);
+        const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
+        const size_t gi = (size_t)t * g.P + n;
+        float q = 0.f;
+        if (i >= 1) q = (i2f(a4.w) + disc * val) - s.PP[n];  // get_qsa - father->pred_value
+        if (l == 0) {
+            d.A()[gi] = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
+            d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
+            if (!is_leaf && dep > md_of(b4.y)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
+            if (i >= 1) d.Q()[gi] = q;
+            sAz[n] = make_float2(val, i2f(a4.w));
+        }
+        if (i >= 1) {
+            pmn = fminf(pmn, q);
+            pmx = fmaxf(pmx, q);
+        }
+    }
+}
+
 // k_tree after barrier (2), run by all four waves (64-node blocks dealt round-robin):
 //  (S1) every node's ucb score under its parent (cnode.cpp:297-335) -- the prior score of waves 2
 //       and 3 plus the value score, min/max-normalised with the joined min/max -- in place of the
@@ -3364,20 +3591,19 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
 
     if (wv == 2 || wv == 3) {
-        // ======== waves 2, 3: stage the node records; then the prior scores after the
-        // back-propagation and the min/max over the visited nodes off the path ========
-        for (int i0 = 0; i0 < ne; i0 += kWave)
-            if (i0 + l < ne) {
-                if (wv == 2) {
-                    glds16a(d.A() + nb + i0 + l, sA + i0);
-                    glds16a(d.Bn() + nb + i0 + l, sB + i0);
-                    glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);
-                } else {
-                    glds4a(d.PP() + nb + i0 + l, sPP + i0);
-                    glds4a(d.Q() + nb + i0 + l, sQ + i0);
-                    glds4a(d.Par() + nb + i0 + l, sPar + i0);
-                }
-            }
+        // ======== waves 2, 3: stage the node records; back-propagate their path levels; then the
+        // prior scores after the back-propagation and the min/max over the visited nodes off the path ========
+        int2 bp0, bp1;
+        bk_path_records(d, t, PS, wv - 1, bp0, bp1);
+        const bool al = (P & 3) == 0;  // the tree's 4-byte arrays start 16-byte aligned
+        if (wv == 2) {
+            dma_dwords(d.A() + nb, lds_addr(smem) + L::oA, 4 * ne, true);
+            dma_dwords(d.Bn() + nb, lds_addr(smem) + L::oB, 4 * ne, true);
+        } else {
+            dma_dwords(d.PP() + nb, lds_addr(smem) + L::oPP, ne, al);
+            dma_dwords(d.Q() + nb, lds_addr(smem) + L::oQ, ne, al);
+            dma_dwords(d.Par() + nb, lds_addr(smem) + L::oPar, ne, al);
+        }
 #ifdef MZ_ABL_LINES  // experiment: MZ_ABL_LINES x 16 extra cache lines in round 1 (value entries, discarded)
         if (wv == 2) {
             const int2 *gVt = (const int2 *)(d.base + (size_t)pl->d.o_V * 256) + (size_t)t * P * pl->g.E;
@@ -3385,31 +3611,58 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         }
 #endif
         if (SEL && !kTreeLevels<NC> && wv == 3) {  // the pUCT factors per parent visit count (no gathers)
-            for (int i0 = 0; i0 < PS; i0 += kWave)
-                if (i0 + l < PS) glds4a(d.pb() + i0 + l, spb + i0);
-            for (int i0 = 0; i0 < 2 * PS; i0 += kWave)
-                if (i0 + l < 2 * PS) glds4a((const int *)d.sq() + i0 + l, (int *)ssq + i0);
+            dma_dwords(d.pb(), lds_addr(smem) + L::oPb, PS, true);
+            dma_dwords(d.sq(), lds_addr(smem) + L::oSq, 2 * PS, true);
         }
-        const int herr = hp0->err, tot = hp0->tot;
+        const int herr = hp0->err, tot = hp0->tot, D = hp0->D;
         if (herr) {
             wait_vm();
             return;
         }
+        Geo g;
+        g.B = B;
+        g.A = A;
+        g.K = gK;
+        g.P = P;
+        g.PS = PS;
+        g.E = pl->g.E;
+        g.one_minus_rho = pl->g.one_minus_rho;
+        d.o_V = pl->d.o_V;
         if (tot > ne)  // slow path: the host bound was too small (a graph replayed out of sequence)
             for (int i0 = ne; i0 < tot; i0 += kWave)
                 if (i0 + l < tot) {
                     if (wv == 2) {
                         glds16a(d.A() + nb + i0 + l, sA + i0);
                         glds16a(d.Bn() + nb + i0 + l, sB + i0);
-                        glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);
+                        glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);  // (wave 0 stages ne)
                     } else {
                         glds4a(d.PP() + nb + i0 + l, sPP + i0);
                         glds4a(d.Q() + nb + i0 + l, sQ + i0);
                         glds4a(d.Par() + nb + i0 + l, sPar + i0);
                     }
                 }
-        wait_vm();
+        // this wave's path levels' value entries: issued last, in flight across barrier (1)
+        const BkPre pre = bk_prestage(d, t, P, g.E, D, wv - 1, bp0, bp1, (int2 *)(smem + L::oReg));
+        wait_vm_but(pre.ndma);
+        stamp(ts, 1);
         lds_barrier();  // (1)
+        stamp(ts, 2);
+        // this wave's path levels first (the back-propagation is the critical path)
+        const float r_in = unif(xf[60]), v_in = unif(xf[61]);  // (wave 1 staged them)
+        Lds s{};
+        s.A = sA;
+        s.B = sB;
+        s.PP = sPP;
+        s.path = sPath;
+        s.lp = sLp;
+        float *boot = (float *)(smem + L::oBoot) + (wv - 1) * (L::PSx + kWave);
+        bk_boot(s, boot, D, v_in, r_in, discount);
+        int berr = 0;
+        long long ber = 0, bew = 0;
+        float bmn, bmx;
+        bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+                  discount, wv - 1, berr, ber, bew, bmn, bmx);
+        stamp(ts, 3);
         // nodes 1 .. tot-1 in 64-node blocks, alternating between the two waves
         constexpr int NBW = (NC + 2 * kWave - 1) / (2 * kWave);
         const float *T = d.T();
@@ -3451,29 +3704,47 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             }
         }
         cv = wave_sum(cv);
-        mn = wave_min_to63(mn);
-        mx = wave_max_to63(mx);
+        mn = fminf(wave_min_to63(mn), bmn);  // (with this wave's path nodes)
+        mx = fmaxf(wave_max_to63(mx), bmx);
         if (l == 63) {
             xf[2 * (wv - 1)] = mn;
             xf[2 * (wv - 1) + 1] = mx;
         }
-        if (l == 0) xi[7 + wv] = cv;
+        if (l == 0) {
+            xi[7 + wv] = cv;
+            xi[9 + wv] = berr;  // (xi[11], xi[12])
+            xl[2 * wv + 7] = ber;  // (xl[11], xl[13])
+            xl[2 * wv + 8] = bew;  // (xl[12], xl[14])
+            if (MZ_STAMPS) {
+                xl[wv + 2] = (long long)(ts[1] - ts[0]);  // (xl[4], xl[5]) arrival at barrier (1)
+                xl[wv + 4] = (long long)(ts[3] - ts[2]);  // (xl[6], xl[7]) its path levels
+                xl[wv + 6] = (long long)(__builtin_amdgcn_s_memtime() - ts[2]);  // (xl[8], xl[9]) all work after (1)
+            }
+        }
         lds_barrier();  // (2)
         if constexpr (SEL && !kTreeLevels<NC>) {
-            const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[14]);
-            tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, pl->g.delta, PS, hp0->D);
+            const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[14]);
+            tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, pl->g.delta, PS, D);
         }
+        wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
     }
 
     if (wv == 1) {
-        // ======== wave 1: the path; then CTree::back_propagate (cnode.cpp:415-450) ========
-        for (int i0 = 0; i0 < 2 * pe; i0 += kWave)
-            if (i0 + l < 2 * pe) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
-        for (int i0 = 0; i0 < PS + 1; i0 += kWave)
-            if (i0 + l < PS + 1) glds4a(d.lp() + i0 + l, sLp + i0);
+        // ======== wave 1: the path; then CTree::back_propagate (cnode.cpp:415-450) of its levels ========
+        int2 bp0, bp1;
+        bk_path_records(d, t, PS, 0, bp0, bp1);
+        dma_dwords(d.path() + (size_t)t * PS, lds_addr(smem) + L::oPath, 2 * pe, (PS & 1) == 0);
+        dma_dwords(d.lp(), lds_addr(smem) + L::oLp, PS + 1, true);
+        unsigned long long tw1[4] = {0};
+        stamp(tw1, 0);
         const int herr = hp0->err, tot = hp0->tot, D = hp0->D;
-        const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
+        // this simulation's reward and value for every wave, through LDS-DMA (a scalar load would
+        // hold up every later LDS wait of the wave behind its two scalar round trips)
+        if (l == 0) {
+            glds4a(reward + t, xf + 60);
+            glds4a(value + t, xf + 61);
+        }
         Geo g;
         g.B = B;
         g.A = A;
@@ -3488,76 +3759,57 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             wait_vm();
             return;
         }
+        stamp(tw1, 1);
         if (D + 1 > pe)
             for (int i0 = 2 * pe; i0 < 2 * (D + 1); i0 += kWave)
                 if (i0 + l < 2 * (D + 1)) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
+        const BkPre pre = bk_prestage(d, t, P, g.E, D, 0, bp0, bp1, (int2 *)(smem + L::oReg));
         const int nf = tot > ne ? tot : ne;  // path-node flags: cleared, then set once the path landed
         for (int i0 = 0; i0 < nf; i0 += kWave)
             if (i0 + l < nf) sFl[i0 + l] = 0;
-        wait_vm();
+        stamp(tw1, 2);
+        wait_vm_but(pre.ndma);  // the path (the entries stay in flight)
+        stamp(tw1, 3);
         for (int i0 = 0; i0 <= D; i0 += kWave)
             if (i0 + l <= D) {
                 const int n = sPath[i0 + l].x;
                 if (n >= 0 && n < tot) sFl[n] = i0 + l + 1;
             }
+        stamp(ts, 2);
         lds_barrier();  // (1)
         stamp(ts, 1);
-        // the path nodes' value-set scalars, then the value entries the updates need
-        // (stage_regions), the bootstrap chain meanwhile
+        const float r_in = unif(xf[60]), v_in = unif(xf[61]);
         Lds s{};
         s.A = sA;
         s.B = sB;
         s.PP = sPP;
         s.path = sPath;
         s.lp = sLp;
-        s.boot = (float *)(smem + L::oBoot);
-        s.reg = (int2 *)(smem + L::oReg);
-        int n0 = 0, nv0 = 0, need0 = 0, off0 = 0;
+        float *boot = (float *)(smem + L::oBoot);
+        bk_boot(s, boot, D, v_in, r_in, discount);
         int err = 0;
-        unsigned long long tsr[3] = {0};
-        stamp(tsr, 2);
-        int acc0 = 0;
-        int cnt0;
-        if constexpr (kTreeFlat<NC>) cnt0 = tree_stage_regions(g, d, s, t, D, 0, n0, nv0, need0, off0, acc0);
-        else cnt0 = stage_regions<true>(g, d, s, t, D, 0, n0, nv0, need0, off0, tsr);
         long long ent_r = 0, ent_w = 0;
         float pmn, pmx;
-        unsigned long long tb[8] = {0};
-        stamp(tb, 0);
-        backup_tree<kTreeFlat<NC>>(g, d, s, sAz, t, D, v_in, r_in, discount, cnt0, n0, nv0, need0, off0, acc0, err, ent_r, ent_w,
-                    pmn, pmx, tb, (const float4 *)(smem + L::oCn));
-        pmn = wave_min_to63(pmn);
-        pmx = wave_max_to63(pmx);
-        for (unsigned long long m = ballot(err != 0); m; m &= m - 1ull) err |= rl(err, __builtin_ctzll(m));  // any lane's
-        if (l == 63) {
+        bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+                  discount, 0, err, ent_r, ent_w, pmn, pmx);
+        if (l == 0) {
             xf[0] = pmn;
             xf[1] = pmx;
-        }
-        if (l == 0) {
             xi[8] = err;
             xl[0] = ent_r;
             xl[1] = ent_w;
             if (MZ_STAMPS) {
-                xl[2] = (long long)(__builtin_amdgcn_s_memtime() - ts[1]);
-                xl[3] = (long long)(tb[0] - ts[1]);
-                xl[4] = (long long)(tb[1] - tb[0]);
-                xl[5] = (long long)(tb[2] - tb[1]);
-                xl[6] = (long long)(tb[6] - tb[2]);
-#if MZ_STAMPS >= 3  // wave 1's staging in detail
-                xl[7] = (long long)(tsr[2] - ts[1]);  // value-set scalars issued
-                xl[8] = (long long)(tsr[0] - tsr[2]);  // path records and need flags read
-                xl[9] = (long long)(tsr[1] - tsr[0]);  // staging offsets
-                xl[10] = (long long)(tb[0] - tsr[1]);  // value entries issued
-#else
-                xl[7] = (long long)(tb[3] - tb[2]);  // first chunk: entry counts
-                xl[8] = (long long)(tb[4] - tb[3]);  // node updates and stores
-                xl[9] = (long long)(tb[5] - tb[4]);  // tail shifts
-#endif
+                xl[2] = (long long)(__builtin_amdgcn_s_memtime() - ts[1]);  // its path levels
+                xl[3] = (long long)(ts[2] - ts[0]);                          // arrival at barrier (1)
+                xl[15] = (long long)(tw1[0] - ts[0]);                        // path / lambda DMA issued
+                xl[16] = (long long)(tw1[1] - tw1[0]);                       // header landed
+                xl[17] = (long long)(tw1[2] - tw1[1]);                       // entries issued
+                xl[18] = (long long)(tw1[3] - tw1[2]);                       // path landed
             }
         }
         lds_barrier();  // (2): its global stores stay in flight
         if constexpr (SEL && !kTreeLevels<NC>) {
-            const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[14]);
+            const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[14]);
             tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, pl->g.delta, PS, D);
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
@@ -3580,6 +3832,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         glds4a(beta + ib, sW);  // (lanes >= A: zero weights, below)
         glds4a(&d.hdr()[t].nxt[l < kNxt ? l : 0], sNxt);
         glds4a((const int *)st + (l < 2 * MZ_S_COUNT ? l : 0), (int *)sSt);
+        // the value-set scalars of the nodes (the back-propagation waves' path nodes read them)
+        for (int i0 = 0; i0 < ne; i0 += kWave)
+            if (i0 + l < ne)
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(d.C() + nb + i0 + l), "s"(lds_addr(smem) + (unsigned)(L::oCn + 16 * i0)) : "memory", "m0");
     }
     const float t00 = ldsc(d.T());  // pb_c(0, 0): the coefficient of the leaf's new children
     TreeHdr h;
@@ -3589,21 +3845,29 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     h.err = hp0->err;
     h.tame = hp0->tame;
     h.leaf = hp0->leaf;
-    const float r_in = ldsc(reward + t), v_in = ldsc(value + t);
     const int gW = pl->g.W;
     const float gdelta = pl->g.delta;
     d.o_D = pl->d.o_D;
     d.o_R = pl->d.o_R;
     const int wbase = h.cursor;
-    {  // the selection's engine words (the expansion's when K > kNxt / 2): always four chunks
+    // the selection's engine words (the expansion's when K > kNxt / 2): word wbase + o is sRng[o + wsh].
+    // One 16-byte chunk per lane from the aligned word below wbase when the window lies inside the
+    // stream (the tree's stream starts 16-byte aligned: W is a multiple of 624), else four dword chunks.
+    const int wsh = ((gW & 3) == 0 && (wbase & ~3) + kRngWin <= gW) ? (wbase & 3) : 0;
+    {
         const unsigned *Rt = d.R() + (size_t)t * gW;
+        if ((gW & 3) == 0 && (wbase & ~3) + kRngWin <= gW) {
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(Rt + (wbase & ~3) + 4 * l), "s"(lds_addr(smem) + (unsigned)L::oRng) : "memory", "m0");
+        } else {
 #pragma unroll
-        for (int i0 = 0; i0 < kRngWin; i0 += kWave) {
-            const int w = wbase + i0 + l;
-            glds4a(Rt + (w < gW ? w : gW - 1), sRng + i0);
+            for (int i0 = 0; i0 < kRngWin; i0 += kWave) {
+                const int w = wbase + i0 + l;
+                glds4a(Rt + (w < gW ? w : gW - 1), sRng + i0);
+            }
         }
     }
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // round 1 landed (the window may not have)
+    if ((gW & 3) == 0 && (wbase & ~3) + kRngWin <= gW) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // round 1 landed (the window may not have)
     unsigned long long tq[4] = {0};
     stamp(tq, 0);
     if (h.err) {  // a dead tree stays dead (every wave reads the same header) and re-reports its error
@@ -3622,10 +3886,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     if (l >= A) sW[l] = 0.f;
     const float pol = sPol[l < A ? l : 0], bet = sW[l < A ? l : 0];
     stamp(ts, 1);
-    // (1) every staged record has landed and the path nodes are flagged: wave 1 back-propagates and
-    // waves 2, 3 score from here on, while this wave expands
+    // (1) every staged record has landed and the path nodes are flagged: waves 1-3 back-propagate
+    // and score from here on, while this wave expands
     lds_barrier();
     stamp(ts, 2);
+    const float r_in = unif(xf[60]), v_in = unif(xf[61]);  // (wave 1 staged them)
     // the sampling distribution and the K draws (std::discrete_distribution, two engine words per
     // draw, cnode.cpp:243-262)
     int cursor = h.cursor;
@@ -3646,8 +3911,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         if (!have_w) wait_vm();  // the words come from the window
         double u = 0.0;
         if (l < K) {
-            const unsigned a1 = have_w ? sNxt[2 * l] : ((2 * l < kRngWin) ? sRng[2 * l] : 0u);
-            const unsigned a2 = have_w ? sNxt[2 * l + 1] : ((2 * l + 1 < kRngWin) ? sRng[2 * l + 1] : 0u);
+            const unsigned a1 = have_w ? sNxt[2 * l] : ((2 * l + wsh < kRngWin) ? sRng[2 * l + wsh] : 0u);
+            const unsigned a2 = have_w ? sNxt[2 * l + 1] : ((2 * l + 1 + wsh < kRngWin) ? sRng[2 * l + 1 + wsh] : 0u);
             u = ((double)a1 + (double)a2 * 4294967296.0) / 18446744073709551616.0;
             if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
         }
@@ -3734,11 +3999,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     stamp(ts, 4);
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
-    err |= uni(xi[8]);
+    err |= uni(xi[8]) | uni(xi[11]) | uni(xi[12]);  // the back-propagation waves
     const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), unif(xf[4]));
     const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), unif(xf[5]));
     const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
-    const long long ent_r = xl[0], ent_w = xl[1];
+    const long long ent_r = xl[0] + xl[11] + xl[13], ent_w = xl[1] + xl[12] + xl[14];
     const int ntot = err ? tot : tot + ncl;
     unsigned long long tp[4] = {0};
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
@@ -3830,8 +4095,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
                         break;
                     }
                     if (cntl > 1) {
-                        const int o = cursor - wbase;
-                        const unsigned w = (o >= 0 && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                        const int o = cursor - wbase + wsh;
+                        const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
                                                                    : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
                         for (int k = uni((int)(w % (unsigned)cntl)); k > 0; --k) lst &= lst - 1ull;
                     }
@@ -3905,8 +4170,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
                         break;
                     }
                     if (cnt > 1) {
-                        const int o = cursor - wbase;
-                        const unsigned w = (o >= 0 && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                        const int o = cursor - wbase + wsh;
+                        const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
                                                                    : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
                         for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
                     }
@@ -3988,9 +4253,9 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     stamp(ts, 7);
     {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
         const int cur = err ? h.cursor : cursor;
-        const int o0 = cur - wbase;
+        const int o0 = cur - wbase + wsh;
         TreeHdr *hp = d.hdr() + t;
-        if (uni((int)(o0 >= 0 && o0 + kNxt <= kRngWin))) {
+        if (uni((int)(o0 >= wsh && o0 + kNxt <= kRngWin))) {
             if (l < kNxt) hp->nxt[l] = sRng[o0 + l];
         } else {  // beyond the window (rare): through LDS-DMA (no compiler wait on the row's loads)
             unsigned *scr = (unsigned *)(smem + L::oIx);
@@ -4033,32 +4298,21 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;    // draws + children
             case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;    // barrier (2) wait
             case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;    // scores + tie lists (4 waves)
-            case MZ_S_CYC_STAGE1: add = (long long)(tp[0] - ts[4]); break;    // (scores)
-            case MZ_S_CYC_W1_SYNC: add = (long long)(tp[1] - tp[0]); break;   // (barrier + tie lists)
-            case MZ_S_CYC_SELECT: add = (long long)(tp[3] - ts[5]); break;    // the chase
-            case MZ_S_CYC_BAK_WAIT: add = (long long)(ts[6] - tp[3]); break;  // path record + outputs
-#if MZ_STAMPS < 3
+            case MZ_S_CYC_STAGE1: add = MZ_STAMPS ? xl[15] : 0; break;       // wave 1: DMA issued
             case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;
-#endif
-            case MZ_S_CYC_EPILOGUE: add = (long long)(ts[8] - ts[7]); break;
+            case MZ_S_CYC_EPILOGUE: add = MZ_STAMPS ? xl[18] : 0; break;     // wave 1: path landed
             case MZ_S_STAMPED: add = 1; break;
-            case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1 after barrier (1)
-#if MZ_STAMPS >= 2  // wave 1's node updates in detail, in place of the expansion's phases
-            case MZ_S_CYC_EXP_CDF: add = xl[7]; break;    // entry counts (first chunk)
-            case MZ_S_CYC_EXP_DRAW: add = xl[8]; break;   // node updates and stores
-            case MZ_S_CYC_EXP_NODES: add = xl[9]; break;  // tail shifts
-#if MZ_STAMPS >= 3
-            case MZ_S_CYC_GATHER: add = xl[10]; break;
-#endif
-#else
-            case MZ_S_CYC_EXP_CDF: add = (long long)(tq[0] - ts[0]); break;   // round 1 landed
-            case MZ_S_CYC_EXP_DRAW: add = (long long)(tq[1] - tq[0]); break;  // sampling distribution
-            case MZ_S_CYC_EXP_NODES: add = (long long)(tq[2] - tq[1]); break; // K draws
-#endif
-            case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? xl[3] : 0; break;       // wave 1: staging issue
-            case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? xl[5] : 0; break;      // wave 1: entries landed
-            case MZ_S_CYC_W1_ROUND1: add = MZ_STAMPS ? xl[6] : 0; break;      // wave 1: node updates
-            case MZ_S_CYC_W1_STAGE2: add = MZ_STAMPS ? xl[4] : 0; break;      // wave 1: bootstrap values
+            case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1: its path levels
+            case MZ_S_CYC_EXP_CDF: add = MZ_STAMPS ? xl[16] : 0; break;      // wave 1: header landed
+            case MZ_S_CYC_EXP_DRAW: add = (long long)(tq[1] - tq[0]); break;  // barrier (1) + distribution
+            case MZ_S_CYC_EXP_NODES: add = MZ_STAMPS ? xl[17] : 0; break;    // wave 1: entries issued
+            case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? xl[3] : 0; break;       // wave 1: arrival at (1)
+            case MZ_S_CYC_W1_STAGE2: add = MZ_STAMPS ? xl[4] : 0; break;      // wave 2: arrival at (1)
+            case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? xl[5] : 0; break;      // wave 3: arrival at (1)
+            case MZ_S_CYC_W1_ROUND1: add = MZ_STAMPS ? xl[6] : 0; break;      // wave 2: its path levels
+            case MZ_S_CYC_W1_SYNC: add = MZ_STAMPS ? xl[7] : 0; break;        // wave 3: its path levels
+            case MZ_S_CYC_SELECT: add = MZ_STAMPS ? xl[8] : 0; break;         // wave 2: all after (1)
+            case MZ_S_CYC_BAK_WAIT: add = MZ_STAMPS ? xl[9] : 0; break;       // wave 3: all after (1)
             default: break;
         }
         st[l] = st_old + add;
@@ -4660,7 +4914,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             }
         if (chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave > 160 * 1024) b->chain_nc = -1;
     }
-    if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && !getenv_flag("MZ_NO_TREE")) b->tree_nc = b->nc;
+    // (k_tree stages one path node's value entries per slot: E <= kBkCap)
+    if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= kBkCap && !getenv_flag("MZ_NO_TREE")) b->tree_nc = b->nc;
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
