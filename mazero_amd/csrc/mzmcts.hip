@@ -183,7 +183,8 @@ __host__ __device__ __forceinline__ void arena_hot(Dev &d, long long B, long lon
     d.o_Q = (unsigned)o; o += arena_span(4 * nodes);
     d.o_PP = (unsigned)o; o += arena_span(4 * nodes);
     d.o_C = (unsigned)o; o += arena_span(16 * nodes);
-    d.o_path = (unsigned)o;
+    d.o_path = (unsigned)o; o += arena_span(8 * (unsigned long long)B * PS);
+    d.o_V = (unsigned)o;  // [P][E] value entries, E = S + 1 = PS - 1
 }
 
 #ifdef MZ_ARGCHECK
@@ -3595,6 +3596,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         // prior scores after the back-propagation and the min/max over the visited nodes off the path ========
         int2 bp0, bp1;
         bk_path_records(d, t, PS, wv - 1, bp0, bp1);
+        const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
         const bool al = (P & 3) == 0;  // the tree's 4-byte arrays start 16-byte aligned
         if (wv == 2) {
             dma_dwords(d.A() + nb, lds_addr(smem) + L::oA, 4 * ne, true);
@@ -3625,9 +3627,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         g.K = gK;
         g.P = P;
         g.PS = PS;
-        g.E = pl->g.E;
-        g.one_minus_rho = pl->g.one_minus_rho;
-        d.o_V = pl->d.o_V;
+        g.E = PS - 1;  // (S + 1)
+        g.one_minus_rho = omr;
         if (tot > ne)  // slow path: the host bound was too small (a graph replayed out of sequence)
             for (int i0 = ne; i0 < tot; i0 += kWave)
                 if (i0 + l < tot) {
@@ -3724,7 +3725,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         lds_barrier();  // (2)
         if constexpr (SEL && !kTreeLevels<NC>) {
             const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[14]);
-            tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, pl->g.delta, PS, D);
+            tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, gdel, PS, D);
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
@@ -3734,6 +3735,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         // ======== wave 1: the path; then CTree::back_propagate (cnode.cpp:415-450) of its levels ========
         int2 bp0, bp1;
         bk_path_records(d, t, PS, 0, bp0, bp1);
+        const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
         dma_dwords(d.path() + (size_t)t * PS, lds_addr(smem) + L::oPath, 2 * pe, (PS & 1) == 0);
         dma_dwords(d.lp(), lds_addr(smem) + L::oLp, PS + 1, true);
         unsigned long long tw1[4] = {0};
@@ -3751,10 +3753,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         g.K = gK;
         g.P = P;
         g.PS = PS;
-        g.E = pl->g.E;
-        g.one_minus_rho = pl->g.one_minus_rho;
-        g.reg_cap = pl->g.reg_cap;
-        d.o_V = pl->d.o_V;
+        g.E = PS - 1;  // (S + 1)
+        g.one_minus_rho = omr;
         if (herr) {
             wait_vm();
             return;
@@ -3810,7 +3810,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         lds_barrier();  // (2): its global stores stay in flight
         if constexpr (SEL && !kTreeLevels<NC>) {
             const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[14]);
-            tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, pl->g.delta, PS, D);
+            tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, gdel, PS, D);
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
@@ -4941,6 +4941,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         plan.dev<float>(d.o_PP, nodes);
         plan.dev<float4>(d.o_C, nodes);
         plan.dev<int2>(d.o_path, (size_t)B * b->PS);
+        plan.dev<int2>(d.o_V, nodes * b->E);
         plan.dev<unsigned>(d.o_R, (size_t)B * b->W);
         plan.dev<float4>(d.o_D, nodes);
         plan.ptr(&b->sel_dev, (size_t)B * (2 + N));
@@ -4948,7 +4949,6 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         b->rb_words = (size_t)2 * B + 2 * (size_t)B * N * A + (size_t)MZ_F_COUNT * B * b->Wd * N;
         if (N > 1) plan.dev<unsigned char>(d.o_J, (size_t)B * g.JP);
         plan.ptr(&b->rb_dev, b->rb_words);
-        plan.dev<int2>(d.o_V, nodes * b->E);
         rc = plan.allocate(b, d);
         if (!rc) {
             Dev chk = d;
@@ -4956,7 +4956,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             const bool same = chk.o_hdr == d.o_hdr && chk.o_stats == d.o_stats && chk.o_err == d.o_err &&
                               chk.o_seed == d.o_seed && chk.o_lp == d.o_lp && chk.o_T == d.o_T && chk.o_pb == d.o_pb &&
                               chk.o_sq == d.o_sq && chk.o_A == d.o_A && chk.o_Par == d.o_Par && chk.o_Bn == d.o_Bn &&
-                              chk.o_Q == d.o_Q && chk.o_PP == d.o_PP && chk.o_C == d.o_C && chk.o_path == d.o_path;
+                              chk.o_Q == d.o_Q && chk.o_PP == d.o_PP && chk.o_C == d.o_C && chk.o_path == d.o_path &&
+                              chk.o_V == d.o_V && b->E == b->PS - 1;
             if (!same || (char *)b->prm != (char *)d.base)
                 rc = fail(MZ_ERR_RUNTIME, "internal: arena layout differs from arena_hot()");
         }
