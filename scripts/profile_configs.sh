@@ -20,6 +20,9 @@ declare -A ARGS=(
   [27m_k5]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5"
 )
 CONFIGS=${CONFIGS:-"3m_k1 3m_k5 2s3z_k1 3s5z_k5 27m_k1 27m_k5"}
+# the PMC passes run first, so the bench lines carry this build's traffic (bench.py reads
+# profiles/pmc_latest.json; on the box that copy is refreshed after every configuration)
+cp profiles/pmc_latest.json gpurun_out/pmc_latest.json 2>/dev/null
 step() {  # log timeout cmd...
     local log=$1 to=$2; shift 2
     timeout -k 10 "$to" "$@" > "$log" 2> "$log.err"
@@ -34,9 +37,6 @@ for c in $CONFIGS; do
     mkdir -p "$d"
     echo "== $c ($a)"
     cpu="--no-cpu"; [ "$c" = 3m_k1 ] && cpu=""
-    step "$d/bench.json" 300 python bench.py $a $cpu
-    step "$d/traced.json" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$d/trace" -o run -- \
-        python3 "$R/bench.py" --no-cpu $a
     # (27m: 27 agent searches x 200 sims = 5,400 fused dispatches per env step; rocprofv3's PMC
     # collection crashed on the host at --steps 3, so those passes profile one step)
     ps="--steps 3 --warmup 1"; case $c in 27m*) ps="--steps 1 --warmup 1";; esac
@@ -46,6 +46,10 @@ for c in $CONFIGS; do
         python3 "$R/bench.py" --no-cpu $ps $a
     step "$d/pmc_summary.txt" 120 python scripts/pmc_summary.py "$d/pmc_fetch" "$d/pmc_write" --bench-args "$a" \
         --out gpurun_out/pmc_latest.json
+    cp gpurun_out/pmc_latest.json profiles/pmc_latest.json
+    step "$d/bench.json" 300 python bench.py $a $cpu
+    step "$d/traced.json" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$d/trace" -o run -- \
+        python3 "$R/bench.py" --no-cpu $a
     # keep the summaries: per-dispatch traces and counter dumps of the 27m workloads are > 64 MiB
     python scripts/reconcile.py gpurun_out/prof --out gpurun_out/prof/summary.json > /dev/null || exit $?
     find "$d" -name "*kernel_trace.csv" -o -name "*counter_collection.csv" | xargs -r rm -f
