@@ -839,7 +839,9 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         }
     }
 #endif
-    __syncthreads();
+    // (the twist exchanges LDS data only: barriers that leave the tempered words' global stores in
+    // flight instead of draining them at every phase)
+    lds_barrier();
     int nb = g.W / kMtN;
 #ifdef MZ_ABL_NOTWIST  // ablation (timing experiments only): no twist / tempering
     nb = 0;
@@ -848,24 +850,24 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         unsigned v = 0;
         // k in [0, 227): x[k] = x[k+397] ^ twist(x[k], x[k+1])       (all old)
         if (tid < 227) v = mt[tid + 397] ^ mt_twist(mt[tid], mt[tid + 1]);
-        __syncthreads();
+        lds_barrier();
         if (tid < 227) mt[tid] = v;
-        __syncthreads();
+        lds_barrier();
         // k in [227, 454): x[k] = x[k-227](new) ^ twist(x[k], x[k+1])(old)
         {
             const int k = 227 + tid;
             if (k < 454) v = mt[k - 227] ^ mt_twist(mt[k], mt[k + 1]);
-            __syncthreads();
+            lds_barrier();
             if (k < 454) mt[k] = v;
-            __syncthreads();
+            lds_barrier();
         }
         // k in [454, 624): x[k] = x[k-227](new) ^ twist(x[k], x[k+1 or 0(new)])
         {
             const int k = 454 + tid;
             if (k < kMtN) v = mt[k - 227] ^ mt_twist(mt[k], (k == kMtN - 1) ? mt[0] : mt[k + 1]);
-            __syncthreads();
+            lds_barrier();
             if (k < kMtN) mt[k] = v;
-            __syncthreads();
+            lds_barrier();
         }
         unsigned *dst = d.R() + (size_t)t * g.W + (size_t)blk * kMtN;
         for (int k = tid; k < kMtN; k += blockDim.x) {
@@ -873,7 +875,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
             dst[k] = z;
             if (blk == 0) w0[k] = z;
         }
-        __syncthreads();
+        lds_barrier();
     }
     if (tid >= kWave) return;
 
