@@ -142,6 +142,11 @@ BIG = [
     ("27m_k1", 256, 36, 1, 200, 0.0),
     ("27m_k5", 256, 36, 5, 200, 0.0),
     ("27m_k8_general_layout", 64, 36, 8, 200, 0.0),  # 1616-node pool: LDS layout from Geo (class 0)
+    # K = 2 trees grow deep paths: k_tree's back-propagation waves handle more than their two
+    # pre-staged levels (later levels staged after the first barrier)
+    ("deep_k2", 64, 9, 2, 200, 0.0),
+    # value sets longer than a k_tree staging slot (E = 401 > kBkCap): the handle falls back to k_step
+    ("k2_long_value_sets", 32, 9, 2, 400, 0.0),
 ]
 
 
