@@ -3327,23 +3327,43 @@ __device__ __forceinline__ void bk_boot(const Lds &s, float *boot, int D, float 
 __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds &s, const float4 *sCn, float2 *sAz,
                                           const float *boot, int2 *sReg, BkPre pre, int t, int D, float reward,
                                           float disc, int k, int &err, long long &ent_r, long long &ent_w, float &pmn,
-                                          float &pmx) {
+                                          float &pmx, unsigned long long *tl = nullptr) {
     const int l = lane_id();
     int2 *gV = d.V() + (size_t)t * g.P * g.E;
     pmn = INFINITY;
     pmx = -INFINITY;
     wait_vm();  // the pre-staged entries (in flight across barrier (1))
+    if (MZ_STAMPS && tl) tl[0] = __builtin_amdgcn_s_memtime();
     for (int j = 0, i = k; i <= D; ++j, i += kBk) {
-        const int2 pe = s.path[i];
-        const int n = uni(pe.x), nv = uni(pe.y);
+        // the level's node: from the pre-stage's scalar path records (no LDS round trip) or the path
+        int n, nv;
+        if (j == 0 && pre.nv0 >= 0) {
+            n = pre.n0;
+            nv = pre.nv0;
+        } else if (j == 1 && pre.nv1 >= 0) {
+            n = pre.n1;
+            nv = pre.nv1;
+        } else {
+            const int2 pe = s.path[i];
+            n = uni(pe.x);
+            nv = uni(pe.y);
+        }
         if (n < 0 || n >= g.P || nv < 0 || nv > kBkCap) {
             err |= kErrPath;
             continue;
         }
+        const int dep = D - i;
+        // every record of the node in one LDS round trip
+        const int4 b4 = s.B[n];
+        const int4 a4r = s.A[n];
+        const float4 cw = sCn[n];
+        const float ppn = s.PP[n];
+        const float lp = s.lp[dep];
+        const float key = boot[i];
         const int2 *R;
-        if (j == 0 && pre.nv0 == nv && pre.n0 == n) {
+        if (j == 0 && pre.nv0 >= 0) {
             R = sReg + (2 * k) * kBkCap;
-        } else if (j == 1 && pre.nv1 == nv && pre.n1 == n) {
+        } else if (j == 1 && pre.nv1 >= 0) {
             R = sReg + (2 * k + 1) * kBkCap;
         } else {  // a later level (or a pre-stage that did not match): slot 0, free once level j - 2 is done
             int2 *dst = sReg + (2 * k) * kBkCap;
@@ -3353,13 +3373,11 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             wait_vm();
             R = dst;
         }
-        const int dep = D - i;
-        const float key = boot[i];
-        const int4 b4 = uni4(s.B[n]);
+        const int by = uni(b4.y);
         // entries of a smaller depth / the same depth / the same depth and a smaller value; none but
         // smaller depths when the node's deepest entry is above dep (stage_regions' need test)
         int lo = nv, c = 0, pv = 0;
-        if (nv > 0 && md_of(b4.y) >= dep) {
+        if (nv > 0 && md_of(by) >= dep) {
             lo = 0;
             for (int e0 = 0; e0 < nv; e0 += kWave) {
                 const bool on = e0 + l < nv;
@@ -3370,9 +3388,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             }
             ent_r += nv;
         }
-        const float4 cw = sCn[n];
         float ws = cw.x, tw = cw.y;
-        const float lp = s.lp[dep];
         const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
         const int nl = value_lim(c + 1, g.one_minus_rho);
         if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
@@ -3411,17 +3427,17 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
         ent_w += nv - pos + 1;
         const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
-        int4 a4 = uni4(s.A[n]);
+        int4 a4 = a4r;
         if (is_leaf) a4.w = f2i(reward);
-        const int nc = is_leaf ? 1 : nc_of(b4.y);
+        const int nc = is_leaf ? 1 : nc_of(by);
         const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
         const size_t gi = (size_t)t * g.P + n;
         float q = 0.f;
-        if (i >= 1) q = (i2f(a4.w) + disc * val) - s.PP[n];  // get_qsa - father->pred_value
+        if (i >= 1) q = (i2f(a4.w) + disc * val) - ppn;  // get_qsa - father->pred_value
         if (l == 0) {
             d.A()[gi] = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
             d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
-            if (!is_leaf && dep > md_of(b4.y)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
+            if (!is_leaf && dep > md_of(by)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(by), dep), b4.z, b4.w);
             if (i >= 1) d.Q()[gi] = q;
             sAz[n] = make_float2(val, i2f(a4.w));
         }
@@ -3429,6 +3445,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             pmn = fminf(pmn, q);
             pmx = fmaxf(pmx, q);
         }
+        if (MZ_STAMPS && tl && j < 2) tl[1 + j] = __builtin_amdgcn_s_memtime();
     }
 }
 
@@ -3789,11 +3806,13 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         s.lp = sLp;
         float *boot = (float *)(smem + L::oBoot);
         bk_boot(s, boot, D, v_in, r_in, discount);
+        unsigned long long tl[4] = {0};
+        stamp(tl, 3);
         int err = 0;
         long long ent_r = 0, ent_w = 0;
         float pmn, pmx;
         bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
-                  discount, 0, err, ent_r, ent_w, pmn, pmx);
+                  discount, 0, err, ent_r, ent_w, pmn, pmx, tl);
         if (l == 0) {
             xf[0] = pmn;
             xf[1] = pmx;
@@ -3803,10 +3822,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             if (MZ_STAMPS) {
                 xl[2] = (long long)(__builtin_amdgcn_s_memtime() - ts[1]);  // its path levels
                 xl[3] = (long long)(ts[2] - ts[0]);                          // arrival at barrier (1)
-                xl[15] = (long long)(tw1[0] - ts[0]);                        // path / lambda DMA issued
-                xl[16] = (long long)(tw1[1] - tw1[0]);                       // header landed
-                xl[17] = (long long)(tw1[2] - tw1[1]);                       // entries issued
-                xl[18] = (long long)(tw1[3] - tw1[2]);                       // path landed
+                xl[15] = (long long)(tl[3] - ts[1]);                         // bootstrap values
+                xl[16] = (long long)(tl[0] - tl[3]);                         // pre-staged entries landed
+                xl[17] = (long long)(tl[1] - tl[0]);                         // level 0 (the root)
+                xl[18] = (long long)(tl[2] - tl[1]);                         // level 3 (when on the path)
             }
         }
         lds_barrier();  // (2): its global stores stay in flight
@@ -4300,14 +4319,14 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;    // draws + children
             case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;    // barrier (2) wait
             case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;    // scores + tie lists (4 waves)
-            case MZ_S_CYC_STAGE1: add = MZ_STAMPS ? xl[15] : 0; break;       // wave 1: DMA issued
+            case MZ_S_CYC_STAGE1: add = MZ_STAMPS ? xl[15] : 0; break;       // wave 1: bootstrap
             case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;
-            case MZ_S_CYC_EPILOGUE: add = MZ_STAMPS ? xl[18] : 0; break;     // wave 1: path landed
+            case MZ_S_CYC_EPILOGUE: add = MZ_STAMPS ? xl[18] : 0; break;     // wave 1: level 3
             case MZ_S_STAMPED: add = 1; break;
             case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1: its path levels
-            case MZ_S_CYC_EXP_CDF: add = MZ_STAMPS ? xl[16] : 0; break;      // wave 1: header landed
+            case MZ_S_CYC_EXP_CDF: add = MZ_STAMPS ? xl[16] : 0; break;      // wave 1: entries landed
             case MZ_S_CYC_EXP_DRAW: add = (long long)(tq[1] - tq[0]); break;  // barrier (1) + distribution
-            case MZ_S_CYC_EXP_NODES: add = MZ_STAMPS ? xl[17] : 0; break;    // wave 1: entries issued
+            case MZ_S_CYC_EXP_NODES: add = MZ_STAMPS ? xl[17] : 0; break;    // wave 1: level 0
             case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? xl[3] : 0; break;       // wave 1: arrival at (1)
             case MZ_S_CYC_W1_STAGE2: add = MZ_STAMPS ? xl[4] : 0; break;      // wave 2: arrival at (1)
             case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? xl[5] : 0; break;      // wave 3: arrival at (1)
