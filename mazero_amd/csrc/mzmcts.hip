@@ -2963,273 +2963,6 @@ int tree_lds_bytes(int nc) {
     }
 }
 
-// k_tree, wave 1: stage_regions with every lane's staging offset (exclusive prefix sum of the
-// needed entry counts, by DPP when the chunk fits reg_cap) and the chunk's entry count acc.
-__device__ __forceinline__ int tree_stage_regions(const Geo &g, const Dev &d, Lds &s, int t, int D, int i0, int &n,
-                                                  int &nv, int &need, int &off, int &acc) {
-    const int l = lane_id();
-    const int i = i0 + l;
-    n = 0;
-    nv = 0;
-    need = 0;
-    if (i <= D) {
-        const int2 pe = s.path[i];
-        n = pe.x;
-        nv = pe.y;
-        need = (nv > 0 && md_of(s.B[n].y) >= D - i) ? 1 : 0;
-    }
-    const int lim = (D + 1 - i0) < kWave ? (D + 1 - i0) : kWave;
-    const int nvs = (l < lim && need) ? nv : 0;
-    const int inc = wave_incl_scan(nvs);
-    const int all = rl(inc, 63);
-    int cnt = lim;
-    if (all <= g.reg_cap) {
-        off = inc - nvs;
-        acc = all;
-    } else {  // (rare) the chunk ends before the first node that would overflow reg_cap
-        int a = 0;
-        off = 0;
-        for (unsigned long long m = ballot(nvs > 0); m; m &= m - 1ull) {
-            const int j = __builtin_ctzll(m);
-            const int vj = rl(nv, j);
-            if (a + vj > g.reg_cap) {
-                cnt = j;
-                break;
-            }
-            if (l >= j) off = a + vj;
-            a += vj;
-        }
-        off -= (l < cnt) ? nvs : 0;
-        if (l >= cnt) {
-            need = 0;
-            off = a;
-        }
-        acc = a;
-    }
-    const int2 *gV = d.V() + (size_t)t * g.P * g.E;
-    int *regdw = (int *)s.reg;
-    for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
-        const int j = __builtin_ctzll(m);
-        const int nj = rl(n, j), dw = 2 * rl(nv, j), oj = rl(off, j);
-        const int *src = (const int *)(gV + (size_t)nj * g.E);
-        for (int c = 0; c < dw; c += kWave)
-            if (c + l < dw) glds4a(src + c + l, regdw + 2 * oj + c);
-    }
-    return cnt;
-}
-
-// bits [a, b) of a 64-bit lane mask, clipped to [0, 64)
-__device__ __forceinline__ unsigned long long lane_range(int a, int b) {
-    a = a < 0 ? 0 : a;
-    b = b > kWave ? kWave : b;
-    if (b <= a) return 0ull;
-    const unsigned long long w = (b - a == kWave) ? ~0ull : ((1ull << (b - a)) - 1ull);
-    return w << a;
-}
-
-// CTree::back_propagate (cnode.cpp:415-450) for k_tree: backup()'s arithmetic and value-entry
-// updates, but the staged node records stay as they were (the prior-score waves read them): the
-// path nodes' new {value, reward} go to sAz, their q values into this wave's min / max, the rest to
-// HBM.  Node n's value-set scalars are sCn[n] (staged with the node records).
-template <bool FLAT>
-__device__ __forceinline__ void backup_tree(const Geo &g, const Dev &d, Lds &s, float2 *sAz, int t,
-                                            int D, float value, float reward, float disc, int cnt0, int n0, int nv0,
-                                            int need0, int off0, int acc0, int &err, long long &ent_r, long long &ent_w,
-                                            float &pmn, float &pmx, unsigned long long *tb, const float4 *sCn) {
-    const int l = lane_id();
-    {  // bootstrap values b_{i-1} = reward_i + discount * b_i (cnode.cpp:424,448), as backup()
-        float carry = value;
-        int hi = D;
-        while (true) {
-            const int lo = hi > 63 ? hi - 63 : 0;
-            const int nl = hi - lo;
-            const int lev = hi - 63 + l;
-            float rn = 0.f;
-            if (lev >= lo && lev < hi) rn = (lev + 1 == D) ? reward : i2f(s.A[s.path[lev + 1].x].w);
-            float b = (l == 63) ? carry : 0.f;
-            float tmp = (l == 62) ? disc * carry : 0.f;
-            boot_dpp(b, tmp, disc, rn, nl);
-            if (lev >= lo && lev <= hi) s.boot[lev] = b;
-            if (lo == 0) break;
-            carry = rlf(b, 63 - nl);
-            hi = lo;
-        }
-    }
-    if (MZ_STAMPS) {
-        wait_lds();
-        stamp(tb, 1);
-    }
-    int2 *gV = d.V() + (size_t)t * g.P * g.E;
-    int cnt = cnt0, n = n0, nv = nv0, need = need0, off = off0, acc = acc0;
-    (void)acc;
-    pmn = INFINITY;
-    pmx = -INFINITY;
-    for (int i0 = 0; i0 <= D;) {
-        if (cnt == 0) {
-            err |= kErrPath;
-            return;
-        }
-        wait_vm();
-        wait_lds();
-        if (MZ_STAMPS && i0 == 0) stamp(tb, 2);
-        const int i = i0 + l;
-        const float key = (l < cnt) ? s.boot[i] : 0.f;
-        int lo = 0, c = 0, pv = 0;  // entries of a smaller depth / the same depth / same depth, smaller value
-        if constexpr (FLAT) {
-            // one lane-parallel pass over the chunk's staged entries: lane e holds entry e and
-            // compares it with its owner node's depth class and key; lane j counts over its own
-            // node's range
-            const unsigned long long own = ballot(l < cnt && need && nv > 0);
-            const int nvs = (l < cnt && need) ? nv : 0;
-            for (int e0 = 0; e0 < acc; e0 += kWave) {
-                const int e = e0 + l;
-                const bool on = e < acc;
-                const int2 en = on ? s.reg[e] : make_int2(0x7fffffff, 0);
-                int od = -1;
-                float ok = 0.f;
-                for (unsigned long long m = own; m; m &= m - 1ull) {
-                    const int j = __builtin_ctzll(m);
-                    if (e >= rl(off, j)) {
-                        od = D - (i0 + j);
-                        ok = rlf(key, j);
-                    }
-                }
-                const unsigned long long blt = ballot(on && en.x < od);
-                const unsigned long long beq = ballot(on && en.x == od);
-                const unsigned long long bpv = ballot(on && en.x == od && i2f(en.y) < ok);
-                const unsigned long long wm = lane_range(off - e0, off + nvs - e0);
-                lo += __popcll(blt & wm);
-                c += __popcll(beq & wm);
-                pv += __popcll(bpv & wm);
-            }
-            if (!need) lo = nv;
-            ent_r += wave_sum(nvs);
-        } else {
-            lo = nv;
-            for (unsigned long long m = ballot(l < cnt && need); m; m &= m - 1ull) {
-                const int j = __builtin_ctzll(m);
-                const int nvj = rl(nv, j), offj = rl(off, j), depj = D - (i0 + j);
-                const float keyj = rlf(key, j);
-                int cl = 0, cc = 0, cp = 0;
-                for (int e0 = 0; e0 < nvj; e0 += kWave) {
-                    const bool on = e0 + l < nvj;
-                    const int2 e = on ? s.reg[offj + e0 + l] : make_int2(0x7fffffff, 0);
-                    cl += __popcll(ballot(on && e.x < depj));
-                    cc += __popcll(ballot(on && e.x == depj));
-                    cp += __popcll(ballot(on && e.x == depj && i2f(e.y) < keyj));
-                }
-                if (l == j) {
-                    lo = cl;
-                    c = cc;
-                    pv = cp;
-                }
-                ent_r += nvj;
-            }
-        }
-        if (MZ_STAMPS && i0 == 0) stamp(tb, 3);
-        int pos = 0;
-        if (l < cnt) {
-            const int dep = D - i;
-            const int2 *R = s.reg + off;
-            const float4 cw = sCn[n];  // (the staged value-set scalars)
-            float ws = cw.x, tw = cw.y;
-            const float lp = s.lp[dep];
-            const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
-            const int nl = value_lim(c + 1, g.one_minus_rho);
-            if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
-                const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
-                if (!(key < mb)) {
-                    ws -= lp * mb;
-                    tw -= lp;
-                    tw += lp;
-                    ws += lp * key;
-                }
-            } else {
-                if (cur + 1 != nl) err |= kErrValueSet;
-                if (c - cur == 0) {
-                    tw += lp;
-                    ws += lp * key;
-                } else {
-                    const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
-                    if (key > ms) {
-                        tw += lp;
-                        ws += lp * key;
-                    } else {
-                        tw += lp;
-                        ws += lp * ms;
-                    }
-                }
-            }
-            pos = lo + pv;
-            int2 *G = gV + (size_t)n * g.E;
-            if (nv + 1 > g.E) {
-                err |= kErrPath;
-                pos = nv;
-            } else {
-                G[pos] = make_int2(dep, f2i(key));
-            }
-            const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
-            int4 a4 = s.A[n];
-            if (is_leaf) a4.w = f2i(reward);
-            const int4 b4 = s.B[n];
-            const int nc = is_leaf ? 1 : nc_of(b4.y);
-            const float val = (nc > 0) ? ws / tw : 0.f;  // CNode::value (cnode.cpp:42-56)
-            const size_t gi = (size_t)t * g.P + n;
-            d.A()[gi] = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
-            d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
-            if (!is_leaf && dep > md_of(b4.y)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(b4.y), dep), b4.z, b4.w);
-            sAz[n] = make_float2(val, i2f(a4.w));
-            if (i >= 1) {
-                const float q = (i2f(a4.w) + disc * val) - s.PP[n];  // get_qsa - father->pred_value
-                d.Q()[gi] = q;
-                pmn = fminf(pmn, q);
-                pmx = fmaxf(pmx, q);
-            }
-        }
-        if (MZ_STAMPS && i0 == 0) stamp(tb, 4);
-        if constexpr (FLAT) {  // the entries at or after each insertion point move up by one, lane-parallel
-            const unsigned long long own = ballot(l < cnt && need && nv > 0);
-            ent_w += wave_sum((l < cnt) ? nv - pos : 0);
-            for (int e0 = 0; e0 < acc; e0 += kWave) {
-                const int e = e0 + l;
-                const int2 en = s.reg[e < acc ? e : 0];
-                int q = -1, pj = 0, nj = 0;
-                for (unsigned long long m = own; m; m &= m - 1ull) {
-                    const int j = __builtin_ctzll(m);
-                    const int oj = rl(off, j);
-                    if (e >= oj) {
-                        q = e - oj;
-                        pj = rl(pos, j);
-                        nj = rl(n, j);
-                    }
-                }
-                if (e < acc && q >= pj) gV[(size_t)nj * g.E + q + 1] = en;
-            }
-        } else {
-            for (unsigned long long m = ballot(l < cnt && nv > pos); m; m &= m - 1ull) {  // tails up by one
-                const int j = __builtin_ctzll(m);
-                const int nvj = rl(nv, j), posj = rl(pos, j), offj = rl(off, j), nj = rl(n, j);
-                ent_w += nvj - posj;
-                int2 *Gj = gV + (size_t)nj * g.E;
-                for (int e0 = posj; e0 < nvj; e0 += kWave)
-                    if (e0 + l < nvj) Gj[e0 + l + 1] = s.reg[offj + e0 + l];
-            }
-        }
-        if (MZ_STAMPS && i0 == 0) stamp(tb, 5);
-        ent_w += cnt;
-        wait_lds();
-        i0 += cnt;
-        if (i0 <= D) {
-            if constexpr (FLAT) cnt = tree_stage_regions(g, d, s, t, D, i0, n, nv, need, off, acc);
-            else cnt = stage_regions<true>(g, d, s, t, D, i0, n, nv, need, off);
-        }
-    }
-    if (MZ_STAMPS) {
-        wait_lds();
-        stamp(tb, 6);
-    }
-}
-
 // ------------------------------------------------------------------------------------------------
 // k_tree's back-propagation on three waves: path level i belongs to wave 1 + i % 3 (kBk waves).
 // A wave stages the value entries of its first two levels before barrier (1), from path records it
@@ -3467,13 +3200,6 @@ constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 // 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
 template <int NC>
 constexpr bool kTreeLevels = (NC >= 1024);
-
-// Wave 1's order statistics as one lane-parallel pass over all staged value entries (lane e
-// holds entry e) up to 384-node pools; larger pools count node by node (their long value sets make
-// the per-entry owner search cost more).  k_tree fused launch, same box: 3m K = 5 10.32 ->
-// 10.09 us (with the staged value-set scalars), 3s5z K = 5 11.88 -> 12.11, 27m K = 5 14.13 -> 15.41.
-template <int NC>
-constexpr bool kTreeFlat = (NC <= 384);
 
 template <int NC>
 __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
