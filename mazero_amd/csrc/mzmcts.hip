@@ -165,26 +165,33 @@ struct Params {
 __host__ __device__ __forceinline__ unsigned long long arena_span(unsigned long long bytes) {
     return (bytes + 64 + 255) / 256;  // ArenaPlan::span, in 256-byte units
 }
-__host__ __device__ __forceinline__ void arena_hot(Dev &d, long long B, long long P, long long PS) {
-    const unsigned long long nodes = (unsigned long long)B * P;
-    const unsigned long long TT = (unsigned long long)(((PS * (PS + 1) / 2) + 3) & ~3ll);
-    unsigned long long o = arena_span(sizeof(Params));
-    d.o_hdr = (unsigned)o; o += arena_span((unsigned long long)B * sizeof(TreeHdr));
-    d.o_stats = (unsigned)o; o += arena_span((unsigned long long)B * MZ_S_COUNT * 8);
-    d.o_err = (unsigned)o; o += arena_span(4);
-    d.o_seed = (unsigned)o; o += arena_span(4);
-    d.o_lp = (unsigned)o; o += arena_span(4 * ((unsigned long long)PS + 1 + kWave));
-    d.o_T = (unsigned)o; o += arena_span(4 * (TT + 4 * kWave));
-    d.o_pb = (unsigned)o; o += arena_span(4 * ((unsigned long long)PS + kWave));
-    d.o_sq = (unsigned)o; o += arena_span(8 * ((unsigned long long)PS + kWave));
-    d.o_A = (unsigned)o; o += arena_span(16 * nodes);
-    d.o_Par = (unsigned)o; o += arena_span(4 * nodes);
-    d.o_Bn = (unsigned)o; o += arena_span(16 * nodes);
-    d.o_Q = (unsigned)o; o += arena_span(4 * nodes);
-    d.o_PP = (unsigned)o; o += arena_span(4 * nodes);
-    d.o_C = (unsigned)o; o += arena_span(16 * nodes);
-    d.o_path = (unsigned)o; o += arena_span(8 * (unsigned long long)B * PS);
-    d.o_V = (unsigned)o;  // [P][E] value entries, E = S + 1 = PS - 1
+// arena_span(c * n + k) in 32-bit arithmetic (c a power of two dividing 256): the kernels compute
+// these offsets in their prologue, where 64-bit scalar pairs cost SGPRs (and spills) on every wave
+template <unsigned c>
+__host__ __device__ __forceinline__ unsigned span_n(unsigned n, unsigned k = 0) {
+    return n / (256 / c) + (c * (n % (256 / c)) + k + 64 + 255) / 256;
+}
+// (mz_create: B < 2^24, B * P < 2^32 and B * PS < 2^32, so every product below fits 32 bits)
+__host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned P, unsigned PS) {
+    const unsigned nodes = B * P;
+    const unsigned TT = ((PS * (PS + 1) / 2) + 3) & ~3u;
+    unsigned o = (unsigned)arena_span(sizeof(Params));
+    d.o_hdr = o; o += (B * (unsigned)sizeof(TreeHdr) + 64 + 255) / 256;
+    d.o_stats = o; o += span_n<8>(B * MZ_S_COUNT);
+    d.o_err = o; o += span_n<4>(1);
+    d.o_seed = o; o += span_n<4>(1);
+    d.o_lp = o; o += span_n<4>(PS + 1 + kWave);
+    d.o_T = o; o += span_n<4>(TT + 4 * kWave);
+    d.o_pb = o; o += span_n<4>(PS + kWave);
+    d.o_sq = o; o += span_n<8>(PS + kWave);
+    d.o_A = o; o += span_n<16>(nodes);
+    d.o_Par = o; o += span_n<4>(nodes);
+    d.o_Bn = o; o += span_n<16>(nodes);
+    d.o_Q = o; o += span_n<4>(nodes);
+    d.o_PP = o; o += span_n<4>(nodes);
+    d.o_C = o; o += span_n<16>(nodes);
+    d.o_path = o; o += span_n<8>(B * PS);
+    d.o_V = o;  // [P][E] value entries, E = S + 1 = PS - 1
 }
 
 #ifdef MZ_ARGCHECK
@@ -4541,6 +4548,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
                                          "agent_num <= 64 and agent_num * action_space_size <= 4096");
     if (S > 65000) return fail(MZ_ERR_UNSUPPORTED, "simulation_num > 65000");
     if (K > 4096) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 4096");
+    if ((long long)B * K * (S + 2) > 0xffffffffll)  // arena_hot's 32-bit offsets (> 256 GiB of node records)
+        return fail(MZ_ERR_UNSUPPORTED, "root_num * sampled_times * (simulation_num + 2) >= 2^32 nodes");
     auto *b = new mz_batch;
     b->B = B;
     b->N = N;
