@@ -3416,7 +3416,9 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, wv - 1, berr, ber, bew, bmn, bmx);
         stamp(ts, 3);
-        // nodes 1 .. tot-1 in 64-node blocks, alternating between the two waves
+        // nodes 1 .. tot-1 in 64-node blocks, alternating between the two waves; wave 3 takes blocks
+        // 0, 2, .. (the odd block count's extra one): its path levels (2, 5, ..) are shallower work
+        // than wave 2's (1, 4, ..)
         constexpr int NBW = (NC + 2 * kWave - 1) / (2 * kWave);
         const float *T = d.T();
         (void)T;
@@ -3425,7 +3427,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         int cv = 0;
 #pragma unroll
         for (int k = 0; k < NBW; ++k) {
-            const int n = (2 * k + wv - 2) * kWave + l;
+            const int n = (2 * k + 3 - wv) * kWave + l;
             pbc[k] = 0.f;
             if (n >= 1 && n < tot) {
                 const int4 a = sA[n];
@@ -3452,7 +3454,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         if constexpr (SEL) {
 #pragma unroll
             for (int k = 0; k < NBW; ++k) {
-                const int n = (2 * k + wv - 2) * kWave + l;
+                const int n = (2 * k + 3 - wv) * kWave + l;
                 if (n >= 1 && n < tot) sPS[n] = pbc[k] * i2f(sA[n].y);  // pb_c * prior (cnode.cpp:316)
             }
         }
@@ -3556,9 +3558,9 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
                 xl[2] = (long long)(__builtin_amdgcn_s_memtime() - ts[1]);  // its path levels
                 xl[3] = (long long)(ts[2] - ts[0]);                          // arrival at barrier (1)
                 xl[15] = (long long)(tl[3] - ts[1]);                         // bootstrap values
-                xl[16] = (long long)(tl[0] - tl[3]);                         // pre-staged entries landed
+                xl[16] = (long long)(tw1[1] - ts[0]);                        // round 1: header landed
                 xl[17] = (long long)(tl[1] - tl[0]);                         // level 0 (the root)
-                xl[18] = (long long)(tl[2] - tl[1]);                         // level 3 (when on the path)
+                xl[18] = (long long)(tw1[3] - tw1[1]);                       // round 1: pre-stage, path landed
             }
         }
         lds_barrier();  // (2): its global stores stay in flight
@@ -4054,10 +4056,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;    // scores + tie lists (4 waves)
             case MZ_S_CYC_STAGE1: add = MZ_STAMPS ? xl[15] : 0; break;       // wave 1: bootstrap
             case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;
-            case MZ_S_CYC_EPILOGUE: add = MZ_STAMPS ? xl[18] : 0; break;     // wave 1: level 3
+            case MZ_S_CYC_EPILOGUE: add = MZ_STAMPS ? xl[18] : 0; break;     // wave 1: pre-stage + path wait
             case MZ_S_STAMPED: add = 1; break;
             case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1: its path levels
-            case MZ_S_CYC_EXP_CDF: add = MZ_STAMPS ? xl[16] : 0; break;      // wave 1: entries landed
+            case MZ_S_CYC_EXP_CDF: add = MZ_STAMPS ? xl[16] : 0; break;      // wave 1: header landed
             case MZ_S_CYC_EXP_DRAW: add = (long long)(tq[1] - tq[0]); break;  // barrier (1) + distribution
             case MZ_S_CYC_EXP_NODES: add = MZ_STAMPS ? xl[17] : 0; break;    // wave 1: level 0
             case MZ_S_CYC_BAK_BOOT: add = MZ_STAMPS ? xl[3] : 0; break;       // wave 1: arrival at (1)
