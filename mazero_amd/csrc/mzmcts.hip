@@ -3486,11 +3486,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     }
 
     if (wv == 1) {
-        // ======== wave 1: the path; then CTree::back_propagate (cnode.cpp:415-450) of its levels ========
+        // ======== wave 1: CTree::back_propagate (cnode.cpp:415-450) of its levels ========
         int2 bp0, bp1;
         bk_path_records(d, t, PS, 0, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
-        dma_dwords(d.path() + (size_t)t * PS, lds_addr(smem) + L::oPath, 2 * pe, (PS & 1) == 0);
         dma_dwords(d.lp(), lds_addr(smem) + L::oLp, PS + 1, true);
         unsigned long long tw1[4] = {0};
         stamp(tw1, 0);
@@ -3514,21 +3513,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             return;
         }
         stamp(tw1, 1);
-        if (D + 1 > pe)
-            for (int i0 = 2 * pe; i0 < 2 * (D + 1); i0 += kWave)
-                if (i0 + l < 2 * (D + 1)) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
         const BkPre pre = bk_prestage(d, t, P, g.E, D, 0, bp0, bp1, (int2 *)(smem + L::oReg));
-        const int nf = tot > ne ? tot : ne;  // path-node flags: cleared, then set once the path landed
-        for (int i0 = 0; i0 < nf; i0 += kWave)
-            if (i0 + l < nf) sFl[i0 + l] = 0;
         stamp(tw1, 2);
-        wait_vm_but(pre.ndma);  // the path (the entries stay in flight)
+        wait_vm_but(pre.ndma);  // the lambda powers, reward and value (the entries stay in flight)
         stamp(tw1, 3);
-        for (int i0 = 0; i0 <= D; i0 += kWave)
-            if (i0 + l <= D) {
-                const int n = sPath[i0 + l].x;
-                if (n >= 0 && n < tot) sFl[n] = i0 + l + 1;
-            }
         stamp(ts, 2);
         lds_barrier();  // (1)
         stamp(ts, 1);
@@ -3583,6 +3571,9 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
     constexpr int kStatN = (MZ_STAMPS != 0) ? MZ_S_COUNT : MZ_S_CYC_HEADER;
     {
+        // the path (the flags below; the back-propagation waves read it after barrier (1)): wave 0
+        // has the slack before barrier (1), wave 1's round 1 is the longest
+        dma_dwords(d.path() + (size_t)t * PS, lds_addr(smem) + L::oPath, 2 * pe, (PS & 1) == 0);
         const size_t ib = (size_t)t * A + (l < A ? l : 0);
         glds4a(policy + ib, sPol);
         glds4a(beta + ib, sW);  // (lanes >= A: zero weights, below)
@@ -3639,6 +3630,21 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         return;
     }
     const int tot = h.tot, D = h.D;
+    if (D + 1 > pe) {  // a path beyond the host bound (a graph replayed out of sequence)
+        for (int i0 = 2 * pe; i0 < 2 * (D + 1); i0 += kWave)
+            if (i0 + l < 2 * (D + 1)) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
+        wait_vm();
+    }
+    {  // path-node flags (1 + path level, else 0): cleared, then set from the staged path
+        const int nf = tot > ne ? tot : ne;
+        for (int i0 = 0; i0 < nf; i0 += kWave)
+            if (i0 + l < nf) sFl[i0 + l] = 0;
+        for (int i0 = 0; i0 <= D; i0 += kWave)
+            if (i0 + l <= D) {
+                const int n = sPath[i0 + l].x;
+                if (n >= 0 && n < tot) sFl[n] = i0 + l + 1;
+            }
+    }
     if (l >= A) sW[l] = 0.f;
     const float pol = sPol[l < A ? l : 0], bet = sW[l < A ? l : 0];
     stamp(ts, 1);
