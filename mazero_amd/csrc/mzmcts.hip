@@ -2985,6 +2985,18 @@ struct BkPre {
     int ndma;              // LDS-DMA instructions issued for them (the wave's last ones before barrier (1))
 };
 
+// The back-propagation's arena offsets as values of this point of the wave (they depend only on
+// the kernel arguments): computed while the wave waits for its round-1 loads, instead of the ~60
+// scalar instructions the compiler otherwise re-derives them with after barrier (1), on the
+// back-propagation's critical path
+__device__ __forceinline__ void bk_pin_offsets(Dev &d) {
+#ifndef MZ_NO_PIN
+    asm volatile("" : "+s"(d.o_V), "+s"(d.o_A), "+s"(d.o_C), "+s"(d.o_Bn), "+s"(d.o_Q));
+#else
+    (void)d;
+#endif
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform n: all but the wave's n most recent vector-memory operations
 __device__ __forceinline__ void wait_vm_but(int n) {
     switch (n) {
@@ -3349,6 +3361,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         int2 bp0, bp1;
         bk_path_records(d, t, PS, wv - 1, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
+        if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
         const bool al = (P & 3) == 0;  // the tree's 4-byte arrays start 16-byte aligned
         if (wv == 2) {
             dma_dwords(d.A() + nb, lds_addr(smem) + L::oA, 4 * ne, true);
@@ -3490,6 +3503,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         int2 bp0, bp1;
         bk_path_records(d, t, PS, 0, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
+        if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
         dma_dwords(d.lp(), lds_addr(smem) + L::oLp, PS + 1, true);
         unsigned long long tw1[4] = {0};
         stamp(tw1, 0);
