@@ -3627,6 +3627,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             }
         }
     }
+    for (int i0 = 0; i0 < ne; i0 += kWave)  // path-node flags cleared while round 1 is in flight
+        if (i0 + l < ne) sFl[i0 + l] = 0;
     if ((gW & 3) == 0 && (wbase & ~3) + kRngWin <= gW) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // round 1 landed (the window may not have)
     unsigned long long tq[4] = {0};
@@ -3649,10 +3651,9 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             if (i0 + l < 2 * (D + 1)) glds4a((const int *)(d.path() + (size_t)t * PS) + i0 + l, (int *)sPath + i0);
         wait_vm();
     }
-    {  // path-node flags (1 + path level, else 0): cleared, then set from the staged path
-        const int nf = tot > ne ? tot : ne;
-        for (int i0 = 0; i0 < nf; i0 += kWave)
-            if (i0 + l < nf) sFl[i0 + l] = 0;
+    {  // path-node flags (1 + path level, else 0): the rest cleared, then set from the staged path
+        for (int i0 = ne; i0 < tot; i0 += kWave)
+            if (i0 + l < tot) sFl[i0 + l] = 0;
         for (int i0 = 0; i0 <= D; i0 += kWave)
             if (i0 + l <= D) {
                 const int n = sPath[i0 + l].x;
