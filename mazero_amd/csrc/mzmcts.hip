@@ -3677,8 +3677,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         cnt = (l == 0) ? K : 0;
     } else {
         double *sp = (double *)(smem + L::oP);
-        double *su = (double *)(smem + L::oU);
-        int *six = (int *)(smem + L::oIx);
         wait_lds();
         const double cp = cdf_staged(A, sW, sp);
         if (MZ_STAMPS) {
@@ -3694,29 +3692,12 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
         }
         if (cursor + 2 * K > gW || 2 * K > kRngWin) err |= kErrRng;
-        sp[l] = cp;
-        su[l] = u;
-        wait_lds();
-        // lower_bound of draw k (lane k): the actions whose cumulative probability is below u_k
-        int ix = 0;
-        for (int a0 = 0; a0 < A; a0 += 8) {
-            double c8[8];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const double2 v = *(const double2 *)(sp + a0 + 2 * q);
-                c8[2 * q] = v.x;
-                c8[2 * q + 1] = v.y;
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) ix += (a0 + j < A && c8[j] < u) ? 1 : 0;
-        }
-        six[l] = ix;
-        wait_lds();
-        // lane a: the draws that chose action a
-        for (int k0 = 0; k0 < K; k0 += 4) {
-            const int4 v = *(const int4 *)(six + k0);
-            cnt += (v.x == l ? 1 : 0) + (k0 + 1 < K && v.y == l ? 1 : 0) + (k0 + 2 < K && v.z == l ? 1 : 0) +
-                   (k0 + 3 < K && v.w == l ? 1 : 0);
+        // draw k's lower_bound (the actions whose cumulative probability is below u_k) as one ballot
+        // over the CDF, one action per lane; lane a counts the draws that chose action a
+        for (int k = 0; k < K; ++k) {
+            const double uk = rld(u, k);
+            const int ix = __popcll(ballot(l < A && cp < uk));
+            cnt += (ix == l) ? 1 : 0;
         }
         cursor += 2 * K;
     }
