@@ -19,10 +19,13 @@ Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every process i
 `python bench.py --gpus N` without torchrun starts the N ranks itself (torch.distributed.run, before
 anything touches the GPU) and n_gpus is the job's world size.  Roots are independent
 (cnode.cpp:633-641), so ranks share no data-path collective:
-  weak   (headline, "scaling": "weak")  every rank searches its own --roots roots (global root
-         offset rank*roots, tree seeds random_seed*2333 + global index);
-  strong (N > 1, reported beside it as "strong_scaling")  the --roots roots split over the ranks.
-`--strong` swaps the two.  The barrier / max-over-ranks clock uses torch.distributed (RCCL).
+  strong (headline, "scaling": "strong")  the metric's --roots (256) roots split over the ranks:
+         rank r searches rows [lo, hi) of the one global batch (global root offset lo, tree seeds
+         random_seed*2333 + global index), so the job is exactly BASELINE.json's 256 roots x 50 sims;
+  weak   (N > 1, reported beside it as "weak_scaling")  every rank searches its own --roots roots
+         (256*N roots in total, a bigger job than the metric names).
+`--weak` swaps the two (the metric string then names the 256*N roots).  The barrier /
+max-over-ranks clock uses torch.distributed (RCCL).
 
 Also reported (rank 0, N=1 only):
   roofline      dominant kernel = the fused simulation step (49 of 52 launches): algorithmic bytes per
@@ -52,6 +55,7 @@ sys.path.insert(0, ROOT)
 import mazero_amd  # noqa: E402,F401  (HIP runtime settings, before anything initialises HIP)
 
 CONFIGS = {  # name: (agents N, actions A) -- smac_maps.py:17-133, n_actions = 6 + n_enemies
+    "matrix": (2, 3),  # BASELINE config #1: config/matrix 2-agent matrix game (matgame.py:16,27-60)
     "3m": (3, 9),
     "2s3z": (5, 11),
     "3s5z_vs_3s6z": (8, 15),
@@ -66,11 +70,11 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--map", default="3m", choices=sorted(CONFIGS))
-    ap.add_argument("--roots", type=int, default=256, help="roots per GPU (weak scaling) / in total (strong)")
+    ap.add_argument("--roots", type=int, default=256, help="roots in total (strong scaling) / per GPU (weak)")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--sampled-times", type=int, default=1, help="K (core/config.py:86 default 1)")
-    ap.add_argument("--strong", action="store_true",
-                    help="headline value from the strong-scaling leg (--roots split over the GPUs)")
+    ap.add_argument("--weak", action="store_true",
+                    help="headline value from the weak-scaling leg (--roots roots on every GPU)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -102,21 +106,21 @@ class HipLeg:
     offset `root_offset`), inputs and network outputs resident in HBM, the whole env step captured
     in one HIP graph."""
 
-    def __init__(self, args, B, root_offset, rank, lib, dev, stream):
+    def __init__(self, args, host_inputs, root_offset, lib, dev, stream):
         import torch
 
         from mazero_amd.cytree import Tree_batch
-        from mazero_amd.synthetic import DEFAULTS, HIDDEN_PER_AGENT, make_search_inputs
+        from mazero_amd.synthetic import DEFAULTS, HIDDEN_PER_AGENT
 
+        B = host_inputs[0].B
         self.args, self.B, self.lib, self.stream = args, B, lib, stream
         N, A = CONFIGS[args.map]
         S, K = args.sims, args.sampled_times
         self.N, self.A, self.S, self.K, self.H = N, A, S, K, N * HIDDEN_PER_AGENT
         d = DEFAULTS
         self.c2, self.c1, self.g = d["pb_c_base"], d["pb_c_init"], d["discount"]
-        # synthetic inputs, one set per agent search, drawn for the global root range of this rank
-        rng = np.random.default_rng(args.seed * 1000 + rank)
-        self.host_inputs = [make_search_inputs(rng, B, A, S) for _ in range(N)]
+        # synthetic inputs, one set per agent search, for this rank's global root range
+        self.host_inputs = host_inputs
 
         def dev_t(a):
             return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -231,10 +235,16 @@ class HipLeg:
                 tb0.expansion_backup_selection_device(s + 1, g, K, sd0["r"][s], sd0["v"][s], sd0["p"][s], sd0["b"][s],
                                                       c2, c1, out=out0, pool=sd0["pool"], gather_out=sd0["leaf"])
         durs = []
+        spans = getattr(self.lib, "mz_debug_spans", None)  # diagnostic builds (MZ_SPANS / MZ_STAMPS) only
+        if spans is not None:
+            spans.argtypes, spans.restype = [C.c_void_p, C.c_int, C.c_int, C.c_int], C.c_int
         with torch.cuda.stream(self.stream):
             for rep in range(6):
                 tb0.prepare(sd0["rr"], sd0["rv"], sd0["rp"], sd0["rb"], K, sd0["eps"], sd0["rn"])
                 tb0.batch_selection_device(c2, c1, g, out=out0)
+                if spans is not None and rep == 5:
+                    torch.cuda.synchronize()
+                    spans(None, 0, 0, 1)
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -246,6 +256,7 @@ class HipLeg:
         torch.cuda.synchronize()
         tb0.synchronize()
         avg = float(np.median(durs))
+        span = launch_spans(spans, S, self.B) if spans is not None else None
         achieved = bytes_per_launch / avg / 1e9
         pmc = pmc_traffic(self.args)
         r = dict(
@@ -263,10 +274,31 @@ class HipLeg:
             avg_launch_us=round(avg * 1e6, 3),
             mean_path_len=round(st["path_edges"] / max(1, st["selects"]), 3),
         )
+        if span is not None:
+            r["launch_span"] = span
         if os.environ.get("MZ_STAMPS") == "1" and st.get("stamped", 0) > 0:
             # diagnostic build: average shader cycles per fused launch and tree, per phase
             r["phase_cycles"] = {k[4:]: round(st[k] / st["stamped"], 1) for k in st if k.startswith("cyc_")}
         return r
+
+
+def launch_spans(spans, S, B):
+    """Diagnostic builds (MZ_SPANS / MZ_STAMPS): the last replay's fused launches (slots hsx = 1 ..
+    S-1) on the chip-wide 100 MHz clock -- body = a launch's earliest wave start to its latest wave
+    end, gap = one launch's latest wave end to the next launch's earliest wave start
+    (mz_debug_spans); body + gap = the back-to-back period the HIP events measure."""
+    slots, trees = min(S, 256), min(B, 1024)
+    buf = (C.c_ulonglong * (2 * slots * trees))()
+    spans(C.cast(buf, C.c_void_p), slots, trees, 0)
+    t = np.array(buf[:], dtype=np.float64).reshape(slots, trees, 2)[1:slots] * 10.0  # ns
+    t0, t1 = t[:, :, 0].min(axis=1), t[:, :, 1].max(axis=1)
+    body = t1 - t0
+    gap = t0[1:] - t1[:-1]
+    return dict(clock="s_memrealtime (100 MHz)", launches=int(len(body)),
+                body_us_mean=round(float(body.mean()) / 1e3, 3), body_us_median=round(float(np.median(body)) / 1e3, 3),
+                gap_us_mean=round(float(gap.mean()) / 1e3, 3), gap_us_median=round(float(np.median(gap)) / 1e3, 3),
+                period_us=round(float(t1[-1] - t0[0]) / 1e3 / len(body), 3),
+                wave_us_mean=round(float((t[:, :, 1] - t[:, :, 0]).mean()) / 1e3, 3))
 
 
 def fused_kernel_name(K: int, P: int) -> str:
@@ -283,18 +315,17 @@ class PortLeg:
     """--backend port (CPU test of the multi-rank plumbing only): the same searches of this rank's
     roots on the host with the CPU port library."""
 
-    def __init__(self, args, B, root_offset, rank):
+    def __init__(self, args, host_inputs, root_offset):
         from mazero_amd import _capi
-        from mazero_amd.synthetic import DEFAULTS, make_search_inputs
+        from mazero_amd.synthetic import DEFAULTS
 
         path = os.path.join(ROOT, "oracle", "_build", "libmzport.so")
         self.lib = _capi.bind(C.CDLL(path))
-        self.args, self.B, self.root_offset = args, B, root_offset
+        self.args, self.B, self.root_offset = args, host_inputs[0].B, root_offset
         N, A = CONFIGS[args.map]
         self.N, self.A, self.S, self.K = N, A, args.sims, args.sampled_times
         self.d = DEFAULTS
-        rng = np.random.default_rng(args.seed * 1000 + rank)
-        self.host_inputs = [make_search_inputs(rng, B, A, self.S) for _ in range(N)]
+        self.host_inputs = host_inputs
         self.graph = None
         self.values = None
 
@@ -321,9 +352,21 @@ class PortLeg:
             self.env_step()
 
 
+def trace_mark(dev, k):
+    """MZ_TRACE_MARKS=1 (profiling runs only): a one-element int16 fill -- FillFunctor<short> in a
+    rocprofv3 kernel trace -- just outside the timed region, so scripts/trace_window.py can cut the
+    timed region's dispatches out of the trace.  Never inside the timed region."""
+    if os.environ.get("MZ_TRACE_MARKS") != "1" or dev.type != "cuda":
+        return
+    import torch
+
+    torch.full((1,), k, dtype=torch.int16, device=dev)
+
+
 def timed(leg, steps, world, dist, sync, dev):
     """EXACTLY `steps` env steps between barrier + device synchronisation on both sides; the max
     over ranks of the wall time."""
+    trace_mark(dev, 1)
     if world > 1:
         dist.barrier()
     sync()
@@ -331,6 +374,7 @@ def timed(leg, steps, world, dist, sync, dev):
     leg.run(steps)
     sync()
     elapsed = time.perf_counter() - t0
+    trace_mark(dev, 2)
     if world > 1:
         import torch
 
@@ -349,7 +393,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from mazero_amd.shard import shard_bounds
+    from mazero_amd.shard import shard_bounds, slice_inputs
+    from mazero_amd.synthetic import make_search_inputs
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -379,25 +424,33 @@ def main():
         lib = load()
         stream = torch.cuda.Stream()
 
-        def make_leg(B, off):
-            return HipLeg(args, B, off, rank, lib, dev, stream)
+        def make_leg(inputs, off):
+            return HipLeg(args, inputs, off, lib, dev, stream)
     else:
-        def make_leg(B, off):
-            return PortLeg(args, B, off, rank)
+        def make_leg(inputs, off):
+            return PortLeg(args, inputs, off)
 
-    # weak scaling: every rank owns --roots roots (global root offset rank * roots)
-    # strong scaling: --roots split over the ranks (only measured separately when world > 1)
+    # strong scaling (headline): the --roots roots of one global batch split over the ranks, rank r
+    #   searching rows [lo, hi) of every agent search's inputs (global root offset lo)
+    # weak scaling: every rank owns --roots roots of its own (global root offset rank * roots)
+    # (one leg at world size 1, where the two are the same job)
     legs = {}
-    order = ["strong", "weak"] if args.strong else ["weak", "strong"]
+    order = ["weak", "strong"] if args.weak else ["strong", "weak"]
     if world == 1:
         order = order[:1]
     for kind in order:
         if kind == "weak":
             B, off, total = args.roots, rank * args.roots, args.roots * world
+            rng = np.random.default_rng(args.seed * 1000 + rank)
+            inputs = [make_search_inputs(rng, B, A, S) for _ in range(N)]
         else:
             lo, hi = shard_bounds(args.roots, world, rank)
             B, off, total = hi - lo, lo, args.roots
-        leg = make_leg(B, off)
+            rng = np.random.default_rng(args.seed * 1000)
+            inputs = [make_search_inputs(rng, args.roots, A, S) for _ in range(N)]
+            if world > 1:
+                inputs = [slice_inputs(inp, lo, hi) for inp in inputs]
+        leg = make_leg(inputs, off)
         leg.prepare()
         st0 = leg.stats() if hip and rank == 0 else None
         elapsed = timed(leg, args.steps, world, dist, sync, dev)
@@ -412,7 +465,8 @@ def main():
         roofline = m["leg"].roofline(m["st0"], m["st1"], args.steps)
     cpu = None
     if hip and rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(m["leg"].host_inputs, m["B"], A, K, S, N, args.cpu_seconds, args.cpu_procs)
+        cpu = cpu_baseline(m["leg"].host_inputs, m["B"], A, K, S, N, args.cpu_seconds, args.cpu_procs,
+                           ptree=args.map == "matrix")
 
     if rank == 0:
         other = {}
@@ -427,9 +481,13 @@ def main():
                 roots_per_gpu=lg["B"],
                 steps=args.steps,
             )
+        if args.map == "3m" and args.roots == 256 and S == 50 and (main_kind == "strong" or world == 1):
+            metric = "MCTS simulations/sec (whole node), SMAC 3m, 256 roots×50 sims, 1/2/4/8 GPUs"
+        else:
+            metric = (f"MCTS simulations/sec (whole node), SMAC {args.map}, {m['total']} roots×{S} sims"
+                      + (f" ({m['B']} per GPU, weak scaling)" if main_kind == "weak" and world > 1 else ""))
         line = {
-            "metric": "MCTS simulations/sec (whole node), SMAC 3m, 256 roots×50 sims, 1/2/4/8 GPUs"
-            if args.map == "3m" else f"MCTS simulations/sec (whole node), SMAC {args.map}",
+            "metric": metric,
             "value": round(value, 1),
             "unit": "simulations/s",
             "n_gpus": world,
@@ -512,10 +570,42 @@ def _cpu_worker(path, shards, B, A, K, S, budget_s, start, q):
     q.put((n_sims, t_run, time.perf_counter() - t0))
 
 
-def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16):
+def ptree_baseline(host_inputs, B, A, K, S, N, budget_s):
+    """BASELINE config #1's "pure-Python ptree" (oracle/ptree.py: the reference ships no Python tree,
+    SURVEY §0): the same env steps through the pure-Python restatement of the ctree, one core, tree
+    calls only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ptree
+
+    from mazero_amd.synthetic import DEFAULTS
+
+    d = DEFAULTS
+    c2, c1, g = d["pb_c_base"], d["pb_c_init"], d["discount"]
+    sims, t_run, steps = 0, 0.0, 0
+    while t_run < budget_s:
+        for inp in host_inputs:
+            tb = ptree.Tree_batch(B, 1, A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"])
+            t0 = time.perf_counter()
+            tb.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps,
+                       inp.root_noise)
+            for s in range(S):
+                tb.batch_selection(c2, c1, g)
+                tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+            tb.get_roots_values()
+            tb.get_roots_marginal_visit_count()
+            t_run += time.perf_counter() - t0
+            sims += B * S
+        steps += 1
+    return {"value": round(sims / t_run, 1), "unit": "simulations/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} env steps x {N} searches x {B} roots x {S} sims (K={K}) = {sims} sims, "
+                      f"{t_run:.1f} s of tree calls, pure-Python ptree (oracle/ptree.py)"}
+
+
+def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
     """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs; plus
     SURVEY §8(d)(ii): the same env steps on several host cores at once, one process per core with
-    the roots sharded over the processes ("multi_core")."""
+    the roots sharded over the processes ("multi_core"); plus, for BASELINE config #1 (`ptree`),
+    the pure-Python ptree on the same env steps."""
     import multiprocessing as mp
 
     from mazero_amd import _capi
@@ -596,6 +686,7 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16):
                   f"{tree_time:.1f} s of tree calls on 1 core of '{cpu_model}' (nproc {os.cpu_count()}, "
                   f"this process's share {len(share)})",
         "multi_core": multi,
+        **({"ptree": ptree_baseline(host_inputs, B, A, K, S, N, budget_s / 2)} if ptree else {}),
     }
 
 

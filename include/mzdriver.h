@@ -59,6 +59,15 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
 int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_agents, int current_agent,
                     const int32_t *factor, int factor_cols, const int32_t *actions, int64_t *joint_out);
 
+/* Census of a captured, not yet instantiated HIP graph (`graph` is a hipGraph_t): its node count
+ * and how many of them are runtime memset nodes.  Under the runtime's default graph packet capture
+ * a replayed hipMemsetAsync node can write a stale fill pattern instead of its value once enough
+ * eager work has run (scripts/memset_graph_repro.py); no mz_* call records one, but
+ * the model's own ops inside a captured search loop might (the reference driver has no graph,
+ * mcts_sampled.py:114-172).  mazero_amd.mcts_sampled runs such a loop eagerly instead of replaying
+ * it. */
+int mz_graph_census(void *graph, int *total_nodes, int *memset_nodes);
+
 #ifdef __cplusplus
 }
 #endif

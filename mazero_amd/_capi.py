@@ -110,6 +110,7 @@ DRIVER_SIGNATURES = {
     "mz_state_changed": (_i, [_p]),
     "mz_policy_glue": (_i, [_p, _p, _i, _i64, _i64, _f, _p, _p]),
     "mz_joint_action": (_i, [_p, _p, _i, _i, _i, _p, _i, _p, _p]),
+    "mz_graph_census": (_i, [_p, C.POINTER(_i), C.POINTER(_i)]),
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 

@@ -19,6 +19,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/mzdriver.h"
 #include "mz_internal.h"
@@ -209,6 +210,28 @@ int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_age
                            (long long *)joint_out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    return MZ_OK;
+}
+
+int mz_graph_census(void *graph, int *total_nodes, int *memset_nodes) {
+    if (!graph || !total_nodes || !memset_nodes) return mz_internal_fail(MZ_ERR_ARG, "mz_graph_census: null argument");
+    hipGraph_t g = (hipGraph_t)graph;
+    size_t n = 0;
+    hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    hipGraphNode_t *nodes = (hipGraphNode_t *)malloc(sizeof(hipGraphNode_t) * (n ? n : 1));
+    if (!nodes) return mz_internal_fail(MZ_ERR_RUNTIME, "mz_graph_census: out of host memory");
+    e = hipGraphGetNodes(g, nodes, &n);
+    int ms = 0;
+    for (size_t k = 0; e == hipSuccess && k < n; ++k) {
+        hipGraphNodeType ty;
+        e = hipGraphNodeGetType(nodes[k], &ty);
+        if (e == hipSuccess && ty == hipGraphNodeTypeMemset) ++ms;
+    }
+    free(nodes);
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    *total_nodes = (int)n;
+    *memset_nodes = ms;
     return MZ_OK;
 }
 

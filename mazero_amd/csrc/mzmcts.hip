@@ -319,6 +319,37 @@ __device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
     if constexpr (MZ_STAMPS != 0) ts[i] = __builtin_amdgcn_s_memtime();
 }
 
+// Launch spans (diagnostic builds, MZ_SPANS=1 or MZ_STAMPS=1): each fused launch's workgroups record
+// their first wave's start and end on the chip-wide 100 MHz clock (s_memrealtime) with one plain
+// 16-byte store per workgroup (no atomics: contended atomics would lengthen the very launch they
+// time), per simulation slot (hsx) and tree.  The host takes min(start) / max(end) per launch:
+// against the HIP-event period of back-to-back launches that splits a launch into its body and
+// the boundary between two kernels (bench.py reads it through mz_debug_spans).
+#ifndef MZ_SPANS
+#define MZ_SPANS MZ_STAMPS
+#endif
+#if MZ_SPANS
+constexpr int kSpanSlots = 256, kSpanTrees = 1024;
+__device__ ulonglong2 g_span[kSpanSlots][kSpanTrees];
+#endif
+__device__ __forceinline__ unsigned long long span_open() {
+#if MZ_SPANS
+    return __builtin_amdgcn_s_memrealtime();
+#else
+    return 0;
+#endif
+}
+__device__ __forceinline__ void span_close(int slot, unsigned long long t0) {
+#if MZ_SPANS
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const int t = blockIdx.x;
+    if (lane_id() == 0 && slot >= 0 && slot < kSpanSlots && t < kSpanTrees) g_span[slot][t] = make_ulonglong2(t0, t1);
+#else
+    (void)slot;
+    (void)t0;
+#endif
+}
+
 // Whole-wave reductions with DPP (no LDS round trips): xor-pairs, xor-quads, half-row and row
 // mirrors reduce each 16-lane row; the four row results are combined from SGPRs.  All lanes must
 // be active.
@@ -2545,6 +2576,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
     const size_t nb = (size_t)t * P;
     unsigned long long ts[8] = {0};
     stamp(ts, 0);
+    const unsigned long long rt0 = span_open();
     // ---- round 1: everything, from the arguments (the chain's length is hsx) ----
     // the header, the leaf's structure record and the handle's constants (scalar loads from the
     // preloaded arena base, issued first; the network outputs follow the LDS-DMA below)
@@ -2904,6 +2936,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
         st[l] = (long long)st_old + add;
     }
     if (l == 0 && err) atomicOr(d.err(), err);
+    span_close(hsx, rt0);
 }
 
 // ================================================================================================
@@ -3352,6 +3385,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     const size_t nb = (size_t)t * P;
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
+    const unsigned long long rt0 = span_open();
     const cTreeHdr *hp0 = (const cTreeHdr *)(d.hdr() + t);
     const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
 
@@ -4076,12 +4110,13 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         st[l] = st_old + add;
     }
     if (l == 0 && err) atomicOr(d.err(), err);
+    span_close(hsx, rt0);
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
 // One device word, set by a kernel.  Captured search graphs never hold a runtime memset node: under
 // the HIP runtime's graph packet capture, a replayed hipMemsetAsync node can write a stale fill
-// pattern once enough ordinary launches have run (scripts/memset_graph_repro.hip).
+// pattern once enough ordinary launches have run (scripts/memset_graph_repro.py).
 __global__ void k_set_word(unsigned *w, unsigned v) { *w = v; }
 
 // Small device-to-device copies of readback fields: one launch of this kernel is cheaper inside
@@ -4803,11 +4838,17 @@ int mz_set_stream(mz_batch *b, void *stream) {
     if (rc) return rc;
     // the new stream waits for the work already queued on the old one (the handle's calls stay in
     // order), except across a graph capture boundary, where the capture itself orders nothing and
-    // an event from outside the capture may not be waited on
+    // an event from outside the capture may not be waited on.  An old stream the runtime no longer
+    // knows (the caller destroyed it: its work was handed to the runtime to finish and the caller
+    // ordered nothing after it) has nothing to order: its error is cleared and the handle switches.
     hipStreamCaptureStatus co = hipStreamCaptureStatusNone, cn = hipStreamCaptureStatusNone;
-    HIP_TRY(hipStreamIsCapturing(b->stream, &co));
     HIP_TRY(hipStreamIsCapturing(ns, &cn));
-    if (co == hipStreamCaptureStatusNone && cn == hipStreamCaptureStatusNone) {
+    bool old_alive = true;
+    if (hipStreamIsCapturing(b->stream, &co) != hipSuccess) {
+        (void)hipGetLastError();
+        old_alive = false;
+    }
+    if (old_alive && co == hipStreamCaptureStatusNone && cn == hipStreamCaptureStatusNone) {
         if (!b->order_ev) HIP_TRY(hipEventCreateWithFlags(&b->order_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(b->order_ev, b->stream));
         HIP_TRY(hipStreamWaitEvent(ns, b->order_ev, 0));
@@ -5172,6 +5213,29 @@ int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *ou
     if (degrees) std::memcpy(degrees, b->rb_host.data() + dego, 4 * (size_t)b->B);
     return MZ_OK;
 }
+
+#if MZ_SPANS
+// diagnostic builds only (not in include/mzmcts.h): reset == 1 zeroes the launch spans; else
+// out[(k * trees + t) * 2 + {0, 1}] = slot k's tree t start / end (100 MHz ticks; 0 = no launch),
+// k < slots <= 256, t < trees <= 1024
+int mz_debug_spans(unsigned long long *out, int slots, int trees, int reset) {
+    static ulonglong2 host[kSpanSlots][kSpanTrees];
+    HIP_TRY(hipDeviceSynchronize());
+    if (reset) {
+        std::memset(host, 0, sizeof(host));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_span), host, sizeof(host)));
+        return MZ_OK;
+    }
+    if (slots > kSpanSlots || trees > kSpanTrees) return fail(MZ_ERR_ARG, "mz_debug_spans: too many slots / trees");
+    HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_span), sizeof(host)));
+    for (int k = 0; k < slots; ++k)
+        for (int t = 0; t < trees; ++t) {
+            out[((size_t)k * trees + t) * 2] = host[k][t].x;
+            out[((size_t)k * trees + t) * 2 + 1] = host[k][t].y;
+        }
+    return MZ_OK;
+}
+#endif
 
 #ifdef MZ_ARGCHECK
 // diagnostic build only: [0] = record count, [1] = kErrPath site bits, then the records

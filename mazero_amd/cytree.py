@@ -52,6 +52,24 @@ def _f32_dev(x):
     return x.contiguous()
 
 
+def _check_out(t, numel: int, dtype, what: str) -> None:
+    """A caller-provided device output of a readback launch: the kernel writes `numel` elements of
+    `dtype` from its data pointer, so anything smaller, of another dtype, strided or on another
+    device would be overwritten out of bounds.  None = field not requested."""
+    if t is None:
+        return
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{what}: a CUDA tensor is required")
+    if t.device.index != torch.cuda.current_device():
+        raise ValueError(f"{what}: on {t.device}, but the tree's device is cuda:{torch.cuda.current_device()}")
+    if t.dtype != dtype:
+        raise ValueError(f"{what}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: must be contiguous")
+    if t.numel() < numel:
+        raise ValueError(f"{what}: {t.numel()} elements, the readback writes {numel}")
+
+
 class Tree_batch:
     """cytree.pyx:7 `cdef class Tree_batch` — one batch of independent sampled-MCTS trees."""
 
@@ -276,11 +294,21 @@ class Tree_batch:
         """Every requested readback of all roots in ONE launch, written into the given device tensors
         (include/mzmcts.h mz_get_roots_device): values [B] f32, marginal_* [B, N, A], degrees [B] int32,
         sampled {field name: [B, max_children(*N)]} as get_roots_sampled_padded_device lays them out."""
+        B, NA = self.root_num, self.agent_num * self.action_space_size
+        W = self.max_children() if sampled else 0
+        _check_out(values, B, torch.float32, "values")
+        _check_out(marginal_visit_count, B * NA, torch.int32, "marginal_visit_count")
+        _check_out(marginal_priors, B * NA, torch.float32, "marginal_priors")
+        _check_out(degrees, B, torch.int32, "degrees")
         o = ReadbackOut()
         ptr = lambda x: None if x is None else x.data_ptr()  # noqa: E731
         o.values, o.marginal_visit_count = ptr(values), ptr(marginal_visit_count)
         o.marginal_priors, o.degrees = ptr(marginal_priors), ptr(degrees)
         for name, t in (sampled or {}).items():
+            if name not in FIELDS:
+                raise ValueError(f"get_roots_device: unknown sampled field {name!r}")
+            width = W * self.agent_num if name == "actions" else W
+            _check_out(t, B * width, torch.int32 if name in INT_FIELDS else torch.float32, f"sampled[{name!r}]")
             o.sampled[FIELDS[name]] = t.data_ptr()
         self._sync_stream()
         check(self._lib, self._lib.mz_get_roots_device(self._h, float(discount), C.byref(o)), "get_roots_device")

@@ -120,7 +120,8 @@ class _SearchLoop:
         self.fac = torch.zeros(B, max(cur, 1), dtype=torch.int32, device=dev)
         self.pool = None
         self.leaf = None
-        self.graph = None
+        self.graph = None  # None: not recorded yet; False: not replayable (capture found memset nodes)
+        self.graph_nodes = None  # (nodes, memset nodes) of the recorded graph
         self.runs = 0
         self.storage = None  # _storage_signature(model) when the loop was made
 
@@ -180,10 +181,29 @@ class _SearchLoop:
             else:
                 tb.batch_expansion_and_backup(s + 1, disc, K, r32, v32, self.probs, self.beta)
 
-    def capture(self, model, cfg, eps, tau):
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+    def capture(self, model, cfg, eps, tau) -> bool:
+        """Record the loop.  The recorded graph is checked before it is instantiated: under the HIP
+        runtime's default graph packet capture a replayed memset node can write a stale fill
+        pattern.  No mz_* call records one, but the model's ops might (a BLAS
+        workspace clear, an output zeroing); then this loop stays eager (graph = False) and the
+        caller runs it eagerly.  Returns whether a graph is ready to replay."""
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g):
             self.run(model, cfg, eps, tau)
+        lib = self.tb._lib
+        total, memsets = C.c_int(0), C.c_int(0)
+        check(lib, lib.mz_graph_census(C.c_void_p(g.raw_cuda_graph()), C.byref(total), C.byref(memsets)),
+              "graph_census")
+        self.graph_nodes = (total.value, memsets.value)
+        if memsets.value:
+            warnings.warn(f"the captured search loop holds {memsets.value} memset node(s) of {total.value} "
+                          "(recorded by the model's ops): a replayed memset node can write a stale value under "
+                          "the HIP runtime's graph packet capture, so this search loop runs eagerly", RuntimeWarning)
+            self.graph = False
+            return False
+        g.instantiate()
+        self.graph = g
+        return True
 
 
 _LOOPS: dict = {}
@@ -337,13 +357,13 @@ class SampledMCTS:
                 st.storage = sig
             st.load(hidden, (rr, rv, rp, rb, rn), factor)
             with torch.no_grad():
-                if not self.use_graph or st.runs == 0:
-                    st.run(model, cfg, eps, sampled_tau)  # eager (the first search also warms up)
-                else:
-                    if st.graph is None:
-                        st.capture(model, cfg, eps, sampled_tau)
+                if self.use_graph and st.runs > 0 and st.graph is None:
+                    st.capture(model, cfg, eps, sampled_tau)  # (records only: nothing runs)
+                if self.use_graph and st.runs > 0 and st.graph:
                     st.graph.replay()
                     tb.state_changed()
+                else:
+                    st.run(model, cfg, eps, sampled_tau)  # eager (the first search also warms up)
                 st.runs += 1
 
             if _host_readback:  # :176-191 (one packed device->host copy)

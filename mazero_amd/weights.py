@@ -26,9 +26,10 @@ import torch.distributed as dist
 
 
 class FlatWeights:
-    """The model's parameters and floating-point buffers, re-homed as views of one flat tensor per
-    dtype (in `named_parameters` / `named_buffers` order, which is identical on every rank for the
-    same architecture)."""
+    """The model's parameters and persistent floating-point buffers -- the floating-point entries of
+    its state_dict -- re-homed as views of one flat tensor per dtype (in `named_parameters` /
+    `named_buffers` order, which is identical on every rank for the same architecture).
+    Non-persistent buffers are not weights (state_dict() leaves them out) and stay where they are."""
 
     def __init__(self, model: torch.nn.Module):
         self.model = model
@@ -36,7 +37,7 @@ class FlatWeights:
         entries = [(m, n, p, True, f"{mn}.{n}" if mn else n) for mn, m in mods for n, p in m._parameters.items()
                    if p is not None]
         entries += [(m, n, b, False, f"{mn}.{n}" if mn else n) for mn, m in mods for n, b in m._buffers.items()
-                    if b is not None and b.is_floating_point()]
+                    if b is not None and b.is_floating_point() and n not in m._non_persistent_buffers_set]
         by_dtype: Dict[torch.dtype, List] = {}
         for e in entries:
             by_dtype.setdefault(e[2].dtype, []).append(e)
@@ -59,7 +60,12 @@ class FlatWeights:
             self.flats[dtype] = flat
 
     def load_into(self, flats: Dict[torch.dtype, torch.Tensor], state_dict) -> None:
-        """Copy a state_dict (the learner's weights) into flat buffers laid out like these."""
+        """Copy a state_dict (the learner's weights) into flat buffers laid out like these.  A
+        DistributedDataParallel learner's keys carry a 'module.' prefix; it is stripped."""
+        if self.index and not set(self.index) & set(state_dict):
+            pre = "module."
+            if all(k.startswith(pre) for k in state_dict):
+                state_dict = {k[len(pre):]: v for k, v in state_dict.items()}
         missing = set(self.index) - set(state_dict)
         if missing:
             raise KeyError(f"state_dict lacks {sorted(missing)[:3]}")
@@ -105,9 +111,16 @@ class WeightBroadcaster:
         """Mark checkpoint `model_index` (SharedStorage.set_weights, core/storage.py:68-80).  With
         `state_dict` (the learner's weights) they are staged and become the live weights -- on this
         rank too -- at the next sync that transfers; without it the live model's current weights
-        are the checkpoint."""
+        are the checkpoint.  That is only consistent when every new index transfers
+        (checkpoint_interval 1): with a longer interval a learner training the source's live model
+        in place would have the source search newer weights than the other ranks until the next
+        crossing, so publishing without a state_dict is refused there (index 0, the initial weights
+        every rank pulls first, excepted)."""
         if dist.get_rank(self.group) != self.src:
             raise RuntimeError("only the source rank publishes weights")
+        if state_dict is None and self.checkpoint_interval > 1 and int(model_index) > 0:
+            raise ValueError("publish() needs the learner's state_dict when checkpoint_interval > 1 (the live "
+                             "model is not a checkpoint between interval crossings)")
         if state_dict is not None:
             if self._stage is None:
                 self._stage = {k: torch.empty_like(v) for k, v in self.flat.flats.items()}

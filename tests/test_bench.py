@@ -17,7 +17,7 @@ def test_defaults_are_the_headline_config():
 
     a = bench.parse([])
     assert (a.map, a.roots, a.sims, a.sampled_times) == ("3m", 256, 50, 1)
-    assert not a.strong and not a.no_graph
+    assert not a.weak and not a.no_graph
 
 
 def test_cpu_baseline_fields(port_lib):
@@ -37,26 +37,51 @@ def test_cpu_baseline_fields(port_lib):
 
 def test_gpus_flag_spawns_ranks(port_lib):
     """`bench.py --gpus 2` without torchrun starts two ranks itself (torch.distributed.run), each
-    rank reports the job's world size, and rank 0 prints one JSON line with the weak (headline) and
-    strong-scaling legs.  --backend port keeps it on the CPU (gloo): the plumbing, not a measurement."""
+    rank reports the job's world size, and rank 0 prints one JSON line.  `value` is the strong leg:
+    the metric's --roots roots split over the ranks (BASELINE.json names 256 roots at 1/2/4/8 GPUs);
+    the weak leg (--roots per rank) rides beside it.  --backend port keeps it on the CPU (gloo): the
+    plumbing, not a measurement."""
     import json
     import subprocess
 
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "port", "--roots", "8",
-           "--sims", "6", "--steps", "2", "--warmup", "1", "--no-cpu"]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "port", "--roots", "8",
+            "--sims", "6", "--steps", "2", "--warmup", "1", "--no-cpu"]
+    r = subprocess.run(base, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["config"]["roots_total"] == 16 and line["config"]["roots_per_gpu"] == 8
-    st = line["strong_scaling"]
-    assert st["roots_total"] == 8 and st["roots_per_gpu"] == 4 and st["value"] > 0
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["roots_total"] == 8 and line["config"]["roots_per_gpu"] == 4
+    assert "8 roots" in line["metric"] and "weak" not in line["metric"]
+    wk = line["weak_scaling"]
+    assert wk["roots_total"] == 16 and wk["roots_per_gpu"] == 8 and wk["value"] > 0
     assert line["value"] > 0
+    # --weak: the weak leg is the headline, under a metric string that names its 16 roots
+    r = subprocess.run(base + ["--weak"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert line["scaling"] == "weak" and line["config"]["roots_total"] == 16
+    assert "16 roots" in line["metric"] and "weak scaling" in line["metric"]
+    assert line["strong_scaling"]["roots_total"] == 8
+
+
+def test_strong_leg_is_the_global_batch(port_lib):
+    """The strong leg's ranks search slices of ONE global batch: rank r's inputs are rows [lo, hi)
+    of the inputs an unsharded run generates (so N > 1 measures the metric's own job)."""
+    import bench
+    from mazero_amd.shard import shard_bounds, slice_inputs
+    from mazero_amd.synthetic import make_search_inputs
+
+    rng = np.random.default_rng(0)
+    full = [make_search_inputs(rng, 10, 9, 4) for _ in range(3)]
+    lo, hi = shard_bounds(10, 4, 1)
+    part = [slice_inputs(x, lo, hi) for x in full]
+    assert part[0].B == hi - lo and np.array_equal(part[2].policy, full[2].policy[:, lo:hi])
+    assert bench.parse(["--gpus", "4"]).roots == 256
 
 
 def test_world_size_mismatch_fails(port_lib):
@@ -68,3 +93,18 @@ def test_world_size_mismatch_fails(port_lib):
            "--sims", "4", "--steps", "1", "--no-cpu"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "--gpus 2" in (r.stderr + r.stdout)
+
+
+def test_matrix_config_ptree_leg(port_lib):
+    """BASELINE config #1 (matrix, N = 2, A = 3, 8 roots x 25 sims): bench.py knows the map and
+    its CPU baseline carries the pure-Python ptree timing beside the ctree's."""
+    import bench
+    from mazero_amd.synthetic import make_search_inputs
+
+    assert bench.CONFIGS["matrix"] == (2, 3)
+    rng = np.random.default_rng(1)
+    B, A, K, S, N = 8, 3, 1, 25, 2
+    inputs = [make_search_inputs(rng, B, A, S) for _ in range(N)]
+    r = bench.cpu_baseline(inputs, B, A, K, S, N, 0.4, procs=2, ptree=True)
+    pt = r["ptree"]
+    assert pt["value"] > 0 and pt["cores"] == 1 and "ptree" in pt["sample"]

@@ -397,7 +397,7 @@ def test_graph_replay_after_eager_launches(port_lib):
     HIP runtime's default graph packet capture.  In round 1 this sequence failed in agent 1's
     replay: the graph then held a hipMemsetAsync node (clearing the error word), and under packet
     capture a replayed memset node wrote a stale fill pattern (0x78787878) once enough ordinary
-    work had run (scripts/memset_graph_repro.hip).  Captured paths now set words with a kernel."""
+    work had run (scripts/memset_graph_repro.py).  Captured paths now set words with a kernel."""
     import torch
 
     from consume import eps_greedy_given, select_action
@@ -438,3 +438,58 @@ def test_graph_replay_after_eager_launches(port_lib):
             acts[i, agent] = eps_greedy_given(got.sampled_actions[i][pos, 0], legal[i, agent], 0.1,
                                               u_eps[agent, i], u_cat[agent, i])
     assert rs_o.random() == rs_d.random()
+
+
+@pytest.mark.gpu
+def test_captured_memset_node_keeps_loop_eager(port_lib):
+    """A model whose forward records a runtime memset node into the captured search loop (here a
+    hipMemsetAsync through ctypes on the capture stream, as a BLAS workspace clear would) is never
+    replayed: under the HIP runtime's packet capture a replayed memset node can write a stale fill
+    (DESIGN.md §7).  The census of the recorded graph (mz_graph_census) finds it, the search warns
+    and runs eagerly, and every search still matches the oracle.  The same loop without the memset
+    records a graph with no memset node and replays it."""
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import _LOOPS, SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, B, S, cur = 3, 9, 32, 10, 0
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=1)
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipMemsetAsync.argtypes = [C.c_void_p, C.c_int, C.c_size_t, C.c_void_p]
+    scratch = torch.empty(64, dtype=torch.int32, device=dev)
+
+    def loop_of(net):
+        return [v for v in _LOOPS.values() if v.model_ref() is net][0]
+
+    for with_memset in (False, True):
+        net = make_net(N, A, seed=51, device=dev)
+        if with_memset:
+            dyn = net.dynamics
+
+            def dynamics(h, a, dyn=dyn):
+                st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+                assert hip.hipMemsetAsync(C.c_void_p(scratch.data_ptr()), 0, 256, st) == 0
+                return dyn(h, a)
+
+            net.dynamics = dynamics
+        rs_o, rs_d = np.random.RandomState(7), np.random.RandomState(7)
+        oracle, drv = OracleSampledMCTS(cfg, rs_o, port_lib), SampledMCTS(cfg, rs_d)
+        for step in range(3):  # eager, capture (+ replay or eager), again
+            out, legal = make_root_batch(net, B, 64, seed=400 + step, device=dev, legal_zero_frac=0.2)
+            exp = oracle.batch_search(net, out, cur, None, N, legal, device=dev, add_noise=True)
+            if with_memset and step == 1:
+                with pytest.warns(RuntimeWarning, match="memset"):
+                    got = drv.batch_search(net, out, cur, None, N, legal, device=dev, add_noise=True)
+            else:
+                got = drv.batch_search(net, out, cur, None, N, legal, device=dev, add_noise=True)
+            _compare_outputs(got, exp)
+        lp = loop_of(net)
+        nodes, memsets = lp.graph_nodes
+        assert nodes > 2 * S
+        if with_memset:
+            assert memsets == S and lp.graph is False
+        else:
+            assert memsets == 0 and isinstance(lp.graph, torch.cuda.CUDAGraph)

@@ -438,3 +438,88 @@ def test_prepare_select_and_one_launch_readback(gpu_lib, port_lib, K):
         e = exp["sampled_" + f]
         gg = t_.cpu().numpy()[:, : e.shape[1]]
         assert np.array_equal(gg.view(np.int32), e.astype(gg.dtype).view(np.int32)), f
+
+
+@pytest.mark.parametrize("path", FULL, ids=[os.path.basename(p)[5:-4] for p in FULL])
+def test_bench_sequence_vs_reference(gpu_lib, path):
+    """bench.py's timed launch sequence, exactly as HipLeg.one_search issues it --
+    mz_prepare_select, (S-1) x mz_expand_backup_select with the leaf-row gather from a pool,
+    mz_expand_backup, one mz_get_roots_device launch -- on every BASELINE-size fixture against the
+    reference ctree's own outputs (oracle/gen_golden.py --full): the selection of every simulation,
+    every field of the one-launch readback, and every gathered row."""
+    from mazero_amd._capi import FIELDS, INT_FIELDS
+    from mazero_amd.synthetic import DEFAULTS
+
+    inp, K, expected = load_full(path)
+    d = to_device(inp)
+    B, A, S = inp.B, inp.A, inp.S
+    c2, c1, g = DEFAULTS["pb_c_base"], DEFAULTS["pb_c_init"], DEFAULTS["discount"]
+    dev = torch.device("cuda")
+    tb = make_tb(gpu_lib, inp, K, {})
+    idx = torch.empty(S, B, dtype=torch.int32, device=dev)
+    idy = torch.empty(S, B, dtype=torch.int32, device=dev)
+    act = torch.empty(S, B, 1, dtype=torch.int32, device=dev)
+    pool = torch.randn(S + 1, B, 96, device=dev)
+    leaf = torch.full((S, B, 96), float("nan"), device=dev)
+    tb.prepare_selection_device(d.root_reward, d.root_value, d.root_policy, d.root_beta, K, d.noise_eps, d.root_noise,
+                                c2, c1, g, out=(idx[0], idy[0], act[0]))
+    for s in range(S):
+        if s + 1 < S:
+            tb.expansion_backup_selection_device(s + 1, g, K, d.reward[s], d.value[s], d.policy[s], d.beta[s], c2, c1,
+                                                 out=(idx[s + 1], idy[s + 1], act[s + 1]), pool=pool,
+                                                 gather_out=leaf[s + 1])
+        else:
+            tb.batch_expansion_and_backup(s + 1, g, K, d.reward[s], d.value[s], d.policy[s], d.beta[s])
+    W = tb.max_children()
+    vals = torch.empty(B, device=dev)
+    mv = torch.empty(B, 1, A, dtype=torch.int32, device=dev)
+    mp = torch.empty(B, 1, A, device=dev)
+    deg = torch.empty(B, dtype=torch.int32, device=dev)
+    sampled = {f: torch.full((B, W), -7, dtype=torch.int32 if f in INT_FIELDS else torch.float32, device=dev)
+               for f in FIELDS}
+    tb.get_roots_device(g, values=vals, marginal_visit_count=mv, marginal_priors=mp, degrees=deg, sampled=sampled)
+    torch.cuda.synchronize()
+    name = os.path.basename(path)
+    assert (idy.cpu().numpy() == np.arange(B, dtype=np.int32)[None]).all()
+    got = dict(sel_idx=idx.cpu().numpy(), sel_act=act.cpu().numpy()[:, :, 0], root_values=vals.cpu().numpy(),
+               marginal_visit_count=mv.cpu().numpy(), marginal_priors=mp.cpu().numpy(), degree=deg.cpu().numpy())
+    assert_same(got, {k: expected[k] for k in got}, f"bench sequence {name} ")
+    dg = got["degree"]
+    for f, t_ in sampled.items():
+        e = expected["sampled_" + f]
+        gg = t_.cpu().numpy()[:, : e.shape[1]].copy()
+        for i in range(B):  # entries past a root's degree are padding (zeros in the fixture)
+            gg[i, dg[i]:] = 0
+        assert_same({f: gg}, {f: e}, f"bench sequence {name} ")
+    # the leaf rows each fused launch gathered: pool[idx_x[i]][i] (mcts_sampled.py:130-134)
+    ix = idx[1:].long()
+    exp_rows = pool[ix, torch.arange(B, device=dev)[None, :]]
+    assert torch.equal(leaf[1:], exp_rows), f"{name}: gathered rows"
+
+
+def test_get_roots_device_checks_outputs(gpu_lib):
+    """get_roots_device refuses caller tensors the readback launch would overrun or misread
+    (ADVICE r2): wrong dtype, too few elements, non-contiguous, host tensors."""
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    inp = make_search_inputs(np.random.default_rng(3), 8, 9, 6)
+    tb = make_tb(gpu_lib, inp, 3, {})
+    run_search(tb, inp, 3, {}, record=False)
+    dev = torch.device("cuda")
+    W = tb.max_children()
+    bad = [
+        dict(values=torch.empty(8, dtype=torch.float64, device=dev)),
+        dict(values=torch.empty(7, device=dev)),
+        dict(marginal_visit_count=torch.empty(8, 1, 9, device=dev)),
+        dict(marginal_priors=torch.empty(8, 9, 2, device=dev)[:, :, 0]),
+        dict(degrees=torch.empty(8, dtype=torch.int32)),
+        dict(sampled={"visit_count": torch.empty(8, W - 1, dtype=torch.int32, device=dev)}),
+        dict(sampled={"priors": torch.empty(8, W, dtype=torch.int32, device=dev)}),
+    ]
+    for kw in bad:
+        with pytest.raises(ValueError):
+            tb.get_roots_device(0.997, **kw)
+    v = torch.empty(8, device=dev)
+    tb.get_roots_device(0.997, values=v, sampled={"visit_count": torch.empty(8, W, dtype=torch.int32, device=dev)})
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy().view(np.int32), tb.get_roots_values().view(np.int32))

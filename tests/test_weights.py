@@ -136,3 +136,61 @@ def test_rccl_broadcast_single_rank():
     ok = q.get(timeout=240)
     p.join(timeout=60)
     assert ok
+
+
+def test_flat_weights_state_dict_keys():
+    """FlatWeights holds exactly the floating-point entries of state_dict(): a non-persistent buffer
+    stays out (state_dict() lacks it, so load_into(model.state_dict()) works); a
+    DistributedDataParallel learner's 'module.'-prefixed state_dict loads too."""
+    from mazero_amd.weights import FlatWeights
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = torch.nn.Linear(4, 3)
+            self.register_buffer("running", torch.zeros(3))
+            self.register_buffer("scratch", torch.ones(5), persistent=False)
+
+    src, dst = M(), M()
+    with torch.no_grad():
+        src.lin.weight.normal_()
+        src.running.fill_(2.0)
+    fw = FlatWeights(dst)
+    assert set(fw.index) == {k for k, v in dst.state_dict().items() if v.is_floating_point()}
+    assert "scratch" not in fw.index and fw.numel == 4 * 3 + 3 + 3
+    fw.load_into(fw.flats, src.state_dict())
+    assert torch.equal(dst.lin.weight, src.lin.weight) and torch.equal(dst.running, src.running)
+    with torch.no_grad():
+        src.lin.bias.add_(1.0)
+    fw.load_into(fw.flats, {"module." + k: v for k, v in src.state_dict().items()})
+    assert torch.equal(dst.lin.bias, src.lin.bias)
+    with pytest.raises(KeyError):
+        fw.load_into(fw.flats, {"lin.weight": src.lin.weight})
+
+
+def test_counter_only_publish_needs_interval_one():
+    """publish(index) without the learner's state_dict makes the live model the checkpoint: fine
+    when every new index transfers (interval 1), refused for a longer interval, where the source
+    would search newer weights than the other ranks between crossings."""
+    import torch.distributed as dist
+
+    from mazero_amd.nets import make_net
+    from mazero_amd.weights import WeightBroadcaster
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        net = make_net(3, 9, seed=5)
+        wb = WeightBroadcaster(net, src=0, checkpoint_interval=1)
+        wb.publish(3)
+        assert wb.sync() == 3
+        wb10 = WeightBroadcaster(make_net(3, 9, seed=6), src=0, checkpoint_interval=10)
+        wb10.publish(0)  # the initial weights are checkpoint 0
+        assert wb10.sync() == 0
+        with pytest.raises(ValueError, match="state_dict"):
+            wb10.publish(12)
+        wb10.publish(12, make_net(3, 9, seed=7).state_dict())
+        assert wb10.sync() == 12
+    finally:
+        dist.destroy_process_group()
