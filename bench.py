@@ -285,20 +285,24 @@ class HipLeg:
 def launch_spans(spans, S, B):
     """Diagnostic builds (MZ_SPANS / MZ_STAMPS): the last replay's fused launches (slots hsx = 1 ..
     S-1) on the chip-wide 100 MHz clock -- body = a launch's earliest wave start to its latest wave
-    end, gap = one launch's latest wave end to the next launch's earliest wave start
-    (mz_debug_spans); body + gap = the back-to-back period the HIP events measure."""
+    end (every wave role that records one), gap = one launch's latest wave end to the next launch's
+    earliest wave start (mz_debug_spans); body + gap = the back-to-back period the HIP events
+    measure.  wave_us: each role's mean end after its workgroup's start."""
     slots, trees = min(S, 256), min(B, 1024)
-    buf = (C.c_ulonglong * (2 * slots * trees))()
+    buf = (C.c_ulonglong * (4 * slots * trees))()
     spans(C.cast(buf, C.c_void_p), slots, trees, 0)
-    t = np.array(buf[:], dtype=np.float64).reshape(slots, trees, 2)[1:slots] * 10.0  # ns
-    t0, t1 = t[:, :, 0].min(axis=1), t[:, :, 1].max(axis=1)
+    t = np.array(buf[:], dtype=np.float64).reshape(slots, trees, 4)[1:slots] * 10.0  # ns
+    start = t[:, :, 0]
+    ends = np.where(t[:, :, 1:] > 0, t[:, :, 1:], np.nan)
+    t0, t1 = start.min(axis=1), np.nanmax(ends, axis=(1, 2))
     body = t1 - t0
     gap = t0[1:] - t1[:-1]
+    wave = {f"w{k}": round(float(np.nanmean(ends[:, :, k] - start)) / 1e3, 3)
+            for k in range(3) if np.isfinite(ends[:, :, k]).any()}
     return dict(clock="s_memrealtime (100 MHz)", launches=int(len(body)),
                 body_us_mean=round(float(body.mean()) / 1e3, 3), body_us_median=round(float(np.median(body)) / 1e3, 3),
                 gap_us_mean=round(float(gap.mean()) / 1e3, 3), gap_us_median=round(float(np.median(gap)) / 1e3, 3),
-                period_us=round(float(t1[-1] - t0[0]) / 1e3 / len(body), 3),
-                wave_us_mean=round(float((t[:, :, 1] - t[:, :, 0]).mean()) / 1e3, 3))
+                period_us=round(float(t1[-1] - t0[0]) / 1e3 / len(body), 3), wave_us=wave)
 
 
 def fused_kernel_name(K: int, P: int) -> str:

@@ -172,11 +172,24 @@ __host__ __device__ __forceinline__ unsigned span_n(unsigned n, unsigned k = 0) 
     return n / (256 / c) + (c * (n % (256 / c)) + k + 64 + 255) / 256;
 }
 // (mz_create: B < 2^24, B * P < 2^32 and B * PS < 2^32, so every product below fits 32 bits)
-__host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned P, unsigned PS) {
+// The node arrays come first: their offsets then follow from B * P alone (k_chain3 computes them
+// with a dozen scalar instructions before its first load).
+__host__ __device__ __forceinline__ void arena_nodes(Dev &d, unsigned B, unsigned P) {
     const unsigned nodes = B * P;
+    const unsigned s16 = span_n<16>(nodes), s4 = span_n<4>(nodes);
+    d.o_A = (unsigned)arena_span(sizeof(Params));
+    d.o_Par = d.o_A + s16;
+    d.o_Bn = d.o_Par + s4;
+    d.o_Q = d.o_Bn + s16;
+    d.o_PP = d.o_Q + s4;
+    d.o_C = d.o_PP + s4;
+    d.o_hdr = d.o_C + s16;
+}
+__host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned P, unsigned PS) {
     const unsigned TT = ((PS * (PS + 1) / 2) + 3) & ~3u;
-    unsigned o = (unsigned)arena_span(sizeof(Params));
-    d.o_hdr = o; o += (B * (unsigned)sizeof(TreeHdr) + 64 + 255) / 256;
+    arena_nodes(d, B, P);
+    unsigned o = d.o_hdr;
+    o += (B * (unsigned)sizeof(TreeHdr) + 64 + 255) / 256;
     d.o_stats = o; o += span_n<8>(B * MZ_S_COUNT);
     d.o_err = o; o += span_n<4>(1);
     d.o_seed = o; o += span_n<4>(1);
@@ -184,12 +197,6 @@ __host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned 
     d.o_T = o; o += span_n<4>(TT + 4 * kWave);
     d.o_pb = o; o += span_n<4>(PS + kWave);
     d.o_sq = o; o += span_n<8>(PS + kWave);
-    d.o_A = o; o += span_n<16>(nodes);
-    d.o_Par = o; o += span_n<4>(nodes);
-    d.o_Bn = o; o += span_n<16>(nodes);
-    d.o_Q = o; o += span_n<4>(nodes);
-    d.o_PP = o; o += span_n<4>(nodes);
-    d.o_C = o; o += span_n<16>(nodes);
     d.o_path = o; o += span_n<8>(B * PS);
     d.o_V = o;  // [P][E] value entries, E = S + 1 = PS - 1
 }
@@ -330,7 +337,7 @@ __device__ __forceinline__ void stamp(unsigned long long *ts, int i) {
 #endif
 #if MZ_SPANS
 constexpr int kSpanSlots = 256, kSpanTrees = 1024;
-__device__ ulonglong2 g_span[kSpanSlots][kSpanTrees];
+__device__ ulonglong2 g_span[kSpanSlots][kSpanTrees][2];  // {wave 0 start, wave 0 end}, {wave 1 end, wave 2 end}
 #endif
 __device__ __forceinline__ unsigned long long span_open() {
 #if MZ_SPANS
@@ -343,10 +350,24 @@ __device__ __forceinline__ void span_close(int slot, unsigned long long t0) {
 #if MZ_SPANS
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     const int t = blockIdx.x;
-    if (lane_id() == 0 && slot >= 0 && slot < kSpanSlots && t < kSpanTrees) g_span[slot][t] = make_ulonglong2(t0, t1);
+    if (lane_id() == 0 && slot >= 0 && slot < kSpanSlots && t < kSpanTrees) g_span[slot][t][0] = make_ulonglong2(t0, t1);
 #else
     (void)slot;
     (void)t0;
+#endif
+}
+// the end of another wave role (1 or 2) of the same launch
+__device__ __forceinline__ void span_end(int slot, int role) {
+#if MZ_SPANS
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const int t = blockIdx.x;
+    if (lane_id() == 0 && slot >= 0 && slot < kSpanSlots && t < kSpanTrees) {
+        unsigned long long *e = (unsigned long long *)&g_span[slot][t][1];
+        e[role - 1] = t1;
+    }
+#else
+    (void)slot;
+    (void)role;
 #endif
 }
 
@@ -2940,6 +2961,586 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
 }
 
 // ================================================================================================
+// K = 1 chains, round 3: three wave roles, the bootstrap recurrence in registers
+// ================================================================================================
+// The same simulation step as k_chain (expansion of the leaf, back-propagation over the chain,
+// min/max normaliser, selection of the new child, leaf-row gather), re-split so that nothing but
+// the expansion and the back-propagation sits on a launch's critical path:
+//  - wave 0 expands the leaf (distribution, draw, the child's records), writes the selection
+//    outputs and, after the one barrier, the header;
+//  - wave 1 back-propagates.  Its node records arrive in registers (lane i = node i).  The
+//    recurrence b_{i-1} = r_i + discount * b_i (cnode.cpp:424,448) runs in registers on every lane
+//    at once (all lanes hold the same b), fed by the chain's rewards read from LDS sixteen at a
+//    time: one dependent multiply + add per level instead of a DPP lane shift;
+//  - wave 2 does what depends only on the header: the leaf-row gather (the next leaf's parent is
+//    this launch's leaf), the next expansion's engine words when the selection is known to take
+//    one word per level (every prior of the leaf's distribution tame: select_walk's fast case
+//    whatever the draw), and the statistics counters.
+// Every error and output is decided from the same scalar inputs as k_chain: results are bit-identical.
+//
+// Launch arguments.  The first 14 dwords arrive preloaded in SGPRs; they hold everything round 1
+// addresses (the node arrays lead the arena, so their offsets follow from B and P: arena_nodes).
+// The outputs (ChainIO) are read through the kernel-argument
+// pointer by the waves that need them, where they need them: the compiler would otherwise load
+// every argument in the common prologue and wait there.  Round 1's scalar loads are issued by
+// inline assembly (sload*) and waited for with one explicit wait (swait): the compiler would sink
+// each load past the first branch after it.
+// --------------------------------------------------------------------------------------------
+struct ChainIO {
+    const char *pool;
+    long long pool_stride, row_bytes;
+    char *gather_out;
+    int *idx_x, *idy, *act;
+};
+struct Chain3Args {  // k_chain3's parameter list, for the kernel-argument offset of ChainIO
+    char *base;
+    const float *policy, *beta, *reward, *value;
+    int ppk, bak, hsx;
+    float discount;
+    ChainIO io;
+};
+static_assert(offsetof(Chain3Args, io) == 56 && sizeof(ChainIO) == 56, "k_chain3 argument layout");
+#ifdef __HIP_DEVICE_COMPILE__
+typedef const __attribute__((address_space(4))) ChainIO cChainIO;
+#else
+typedef const ChainIO cChainIO;
+#endif
+
+typedef int int4v __attribute__((ext_vector_type(4)));
+typedef int int8v __attribute__((ext_vector_type(8)));
+typedef int int16v __attribute__((ext_vector_type(16)));
+// scalar loads issued here and waited for by swait (invisible to the compiler's wait counting, which
+// stays correct: its own LDS waits only ever wait longer with more loads outstanding)
+__device__ __forceinline__ int sload1(const void *p) {
+    int v;
+    asm volatile("s_load_dword %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+typedef int int2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int2v sload2(const void *p) {
+    int2v v;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ uintptr_t u64_of(int lo, int hi) {
+    return (uintptr_t)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ int4v sload4(const void *p) {
+    int4v v;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ int8v sload8(const void *p) {
+    int8v v;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ int16v sload16(const void *p) {
+    int16v v;
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+
+template <int NC>
+struct Chain3Layout {
+    int oW, oP, oRv, oBv, oA, oPP, oX, total;
+    __host__ __device__ static constexpr int r16(int x) { return (x + 15) & ~15; }
+    __host__ __device__ constexpr Chain3Layout(int P)
+        : oW(0),                         // float[64]  the leaf's weights (distribution broadcast)
+          oP(4 * kWave),                 // double[64] its probabilities
+          oRv(oP + 8 * kWave),           // float[P + 32]  rewards reversed: [j] = r_{D-j}
+          oBv(oRv + r16(4 * (P + 32))),  // float[P + 32]  bootstrap values: [j] = b_{D-1-j}
+          oA(oBv + r16(4 * (P + 32))),   // int4[P + 1]    node records after the back-propagation
+          oPP(oA + r16(16 * (P + 1))),   // float[P + 1]   parents' pred_value
+          oX(oPP + r16(4 * (P + 1))),    // min, max, wave 2's flag, v_in; stamps from 64
+          total(oX + 128) {}
+};
+int chain3_lds_bytes(int nc) { return Chain3Layout<0>(nc).total; }
+
+// ROW: the leaf-row gather's class -- 0 any row (copied after the barrier), 1 16-byte aligned rows of
+// <= 4 KiB (registers), 2 aligned rows of <= 16 KiB (LDS-DMA), 3 no gather (no pool, or no selection)
+template <int NC, bool SEL, int ROW>
+__global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy, const float *beta, const float *reward,
+                                                const float *value, int ppk, int bak, int hsx, float discount,
+                                                ChainIO io) {
+    static_assert(NC >= kWave && NC % kWave == 0, "k_chain3 node classes are whole waves");
+    (void)io;  // (read through the kernel-argument pointer, see above)
+    constexpr int NCH = NC / kWave;  // node chunks of one wave
+    constexpr Chain3Layout<NC> L(NC);
+    const int P = ppk & 0xffff, PS = (int)((unsigned)ppk >> 16);
+    const int A = (bak >> 24) & 0x7f, fast_ok = (int)((unsigned)bak >> 31);
+    const int B = bak & 0xffffff;
+    Dev d;
+    d.base = (gchar *)base;
+    arena_nodes(d, B, P);
+    cChainIO *iop = (cChainIO *)((const char *)__builtin_amdgcn_kernarg_segment_ptr() + offsetof(Chain3Args, io));
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float *sX = (float *)(smem + L.oX);
+    int *sXi = (int *)(smem + L.oX);
+    long long *sXl = (long long *)(smem + L.oX + 64);
+    int4 *sA = (int4 *)(smem + L.oA);
+    float *sPP = (float *)(smem + L.oPP);
+    float *sRv = (float *)(smem + L.oRv);
+    float *sBv = (float *)(smem + L.oBv);
+    const int t = blockIdx.x;
+    const int l = threadIdx.x & (kWave - 1);
+    const int wv = uni((int)(threadIdx.x >> 6));
+    const size_t nb = (size_t)t * P;
+    unsigned long long ts[8] = {0};
+    stamp(ts, 0);
+    const unsigned long long rt0 = span_open();
+    TreeHdr *hp = d.hdr() + t;
+    const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
+    const int Dp = (hsx >= 0 && hsx + 1 <= P) ? hsx : 0;  // the chain's leaf, if the header agrees
+
+    if (wv == 1) {
+        // ======== wave 1: CTree::back_propagate (cnode.cpp:415-450) over the chain ========
+        int8v hv = sload8(hp);  // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf
+        int r_i = sload1(reward + t), v_i = sload1(value + t);
+        int o_lp = sload1(&pl->d.o_lp);
+        int4 a4[NCH];
+        float2 cw[NCH];
+        float pp[NCH], lpv[NCH];
+        auto load = [&](int D, const float *lp) {
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const int i = c * kWave + l;
+                a4[c] = make_int4(0, 0, 0, 0);
+                cw[c] = make_float2(0.f, 0.f);
+                pp[c] = 0.f;
+                lpv[c] = 0.f;
+                if (i <= D) {
+                    a4[c] = d.A()[nb + i];
+                    cw[c] = *(const float2 *)&d.C()[nb + i];
+                    pp[c] = d.PP()[nb + i];
+                    lpv[c] = lp[D - i];  // lambda^(D - i): this back-propagation's depth at node i
+                }
+            }
+        };
+        // (lp's offset arrives with the header: the node records go first)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = c * kWave + l;
+            a4[c] = make_int4(0, 0, 0, 0);
+            cw[c] = make_float2(0.f, 0.f);
+            pp[c] = 0.f;
+            if (i <= Dp) {
+                a4[c] = d.A()[nb + i];
+                cw[c] = *(const float2 *)&d.C()[nb + i];
+                pp[c] = d.PP()[nb + i];
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(hv), "+s"(r_i), "+s"(v_i), "+s"(o_lp)::"memory");
+        const float *lpt = (const float *)(base + (size_t)(unsigned)o_lp * 256);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = c * kWave + l;
+            lpv[c] = (i <= Dp) ? lpt[Dp - i] : 0.f;
+        }
+        const float r_in = i2f(r_i), v_in = i2f(v_i);
+        const int herr = hv[3], D = hv[2], toth = hv[1], leafh = hv[7];
+        if (herr) return;  // (wave 0 reports; no wave takes the barrier on the error paths)
+        if (D != Dp || toth != D + 1 || leafh != D) {
+            if (D + 1 > P || toth != D + 1 || leafh != D) return;  // not a chain (wave 0 reports)
+            load(D, lpt);  // a graph replayed out of sequence: the header's chain
+        }
+        const float g = discount;
+        // the chain's rewards, reversed: sRv[j] = r_{D-j} (r_D = this simulation's reward)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = c * kWave + l;
+            if (i >= 1 && i <= D) sRv[D - i] = (i == D) ? r_in : i2f(a4[c].w);
+        }
+        wait_lds();
+        stamp(ts, 1);
+        // b_{D-1-j} = r_{D-j} + discount * b_{D-j}, j = 0 .. D-1, sixteen levels per LDS round
+        // (the next sixteen rewards are read while these run; levels past the root compute values
+        // nobody reads: sRv / sBv are padded)
+        {
+            float b = v_in;
+            float4 n0 = *(const float4 *)(sRv), n1 = *(const float4 *)(sRv + 4), n2 = *(const float4 *)(sRv + 8),
+                   n3 = *(const float4 *)(sRv + 12);
+            for (int j0 = 0; j0 < D; j0 += 16) {
+                const float4 c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+                n0 = *(const float4 *)(sRv + j0 + 16);
+                n1 = *(const float4 *)(sRv + j0 + 20);
+                n2 = *(const float4 *)(sRv + j0 + 24);
+                n3 = *(const float4 *)(sRv + j0 + 28);
+                float4 o0, o1, o2, o3;
+                b = c0.x + g * b; o0.x = b;
+                b = c0.y + g * b; o0.y = b;
+                b = c0.z + g * b; o0.z = b;
+                b = c0.w + g * b; o0.w = b;
+                b = c1.x + g * b; o1.x = b;
+                b = c1.y + g * b; o1.y = b;
+                b = c1.z + g * b; o1.z = b;
+                b = c1.w + g * b; o1.w = b;
+                b = c2.x + g * b; o2.x = b;
+                b = c2.y + g * b; o2.y = b;
+                b = c2.z + g * b; o2.z = b;
+                b = c2.w + g * b; o2.w = b;
+                b = c3.x + g * b; o3.x = b;
+                b = c3.y + g * b; o3.y = b;
+                b = c3.z + g * b; o3.z = b;
+                b = c3.w + g * b; o3.w = b;
+                *(float4 *)(sBv + j0) = o0;
+                *(float4 *)(sBv + j0 + 4) = o1;
+                *(float4 *)(sBv + j0 + 8) = o2;
+                *(float4 *)(sBv + j0 + 12) = o3;
+            }
+        }
+        wait_lds();
+        stamp(ts, 2);
+        // ---- every node of the chain, lane i = node i: visits, value set (an append to an empty
+        // depth class, utils.cpp:36-44), value (cnode.cpp:42-56); min / max over the q of 1..D ----
+        float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const int i = c * kWave + l;
+            if (i <= D) {
+                const float key = (i == D) ? v_in : sBv[D - 1 - i];
+                const float rw = (i == D) ? r_in : i2f(a4[c].w);  // the leaf's reward is this simulation's
+                const float tw = cw[c].y + lpv[c];
+                const float ws = cw[c].x + lpv[c] * key;
+                const float val = ws / tw;
+                const int4 na = make_int4(a4[c].x + 1, a4[c].y, f2i(val), f2i(rw));
+                d.A()[nb + i] = na;
+                *(float2 *)&d.C()[nb + i] = make_float2(ws, tw);
+                sA[i] = na;
+                sPP[i] = pp[c];
+                if (i >= 1) {
+                    const float q = (rw + g * val) - pp[c];  // get_qsa - father->pred_value
+                    mn = fminf(mn, q);
+                    mx = fmaxf(mx, q);
+                }
+            }
+        }
+        mn = unif(rlf(wave_min_to63(mn), 63));
+        mx = unif(rlf(wave_max_to63(mx), 63));
+        if (l == 0) {
+            sX[0] = mn;
+            sX[1] = mx;
+            if (MZ_STAMPS) {
+                sXl[0] = (long long)(ts[2] - ts[1]);                         // the recurrence
+                sXl[1] = (long long)(__builtin_amdgcn_s_memtime() - ts[2]);  // node updates
+                sXl[2] = (long long)(ts[1] - ts[0]);                         // round 1
+            }
+        }
+        lds_barrier();
+        span_end(hsx, 1);
+        return;
+    }
+
+    if (wv == 2) {
+        // ======== wave 2: the leaf-row gather, the next expansion's engine words, the counters ========
+        // Straight-line code in issue order (the row class ROW is a template argument): every wait
+        // the compiler places then counts exactly the loads issued after the one it needs.
+        const float pol = policy[(size_t)t * A + (l < A ? l : 0)];
+        const float bet = beta[(size_t)t * A + (l < A ? l : 0)];
+        // (one scalar round trip: the outputs' kernel arguments, the header, the handle's constants)
+        int8v io8 = sload8((const void *)iop);  // pool, pool_stride, row_bytes, gather_out
+        int16v hv = sload16(hp);                // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf, tame, ...
+        int rv0 = sload1(&d.A()[nb].x), r_i = sload1(reward + t), v_i = sload1(value + t);
+        int gWi = sload1(&pl->g.W), omri = sload1(&pl->g.one_minus_rho), oRi = sload1(&pl->d.o_R);
+        int osti = sload1(&pl->d.o_stats);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+s"(io8), "+s"(hv), "+s"(rv0), "+s"(r_i), "+s"(v_i), "+s"(gWi), "+s"(omri), "+s"(oRi), "+s"(osti)
+                     :
+                     : "memory");
+        stamp(ts, 1);
+        // (typed as global memory: flat accesses would count against lgkmcnt too)
+        const char *pool = (const char *)(const gchar *)u64_of(io8[0], io8[1]);
+        const long long pool_stride = (long long)u64_of(io8[2], io8[3]);
+        const long long row_bytes = (long long)u64_of(io8[4], io8[5]);
+        char *gather_out = (char *)(gchar *)u64_of(io8[6], io8[7]);
+        const int cur0 = hv[0], toth = hv[1], D = hv[2], herr = hv[3], leafh = hv[7], htame = hv[8];
+        const int root_vis0 = rv0;
+        const float r_in = i2f(r_i), v_in = i2f(v_i);
+        const int gW = gWi;
+        const float omr = i2f(omri);
+        // the row of this launch's leaf (hidden_state_index_x = hsx), issued first
+        const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
+        const long long last = row_bytes - 16, o = (long long)l * 16;
+        unsigned char *sbig = smem + L.total;  // (ROW 2: 16 KiB past the layout)
+        int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+        if constexpr (ROW == 1) {  // up to 4 KiB: four 16-byte registers per lane, offsets clamped into the row
+            gv0 = *(const int4 *)(src + (o < last ? o : last));
+            gv1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
+            gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
+            gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
+        } else if constexpr (ROW == 2) {  // up to 16 KiB: sixteen LDS-DMA chunks of 1 KiB
+#pragma unroll
+            for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+        }
+        d.o_stats = (unsigned)osti;
+        long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
+        const long long st_old = st[l < MZ_S_CYC_HEADER ? l : 0];
+        // the engine words after this launch's draw and selection, when select_walk's fast case is
+        // certain (every prior the expansion can create tame: whatever the draw); clamped addresses
+        const int Ds = D + 1;
+        const int words = SEL ? Ds - ((root_vis0 + 1 <= 1) ? 1 : 0) : 0;
+        const int cur = cur0 + ((A >= 2) ? 2 : 0) + words;
+        const unsigned *Rt = (const unsigned *)(base + (size_t)(unsigned)oRi * 256) + (size_t)t * gW;
+        const int wi = cur + l;
+        const unsigned w_raw = Rt[(wi >= 0 && wi < gW) ? wi : 0];
+        // a dead or inconsistent tree: wave 0 reports; no wave takes the barrier on these paths (all
+        // three read the same header)
+        if (herr || D + 1 > P || toth != D + 1 || leafh != D) {
+            wait_vm();  // (no LDS-DMA may land after the workgroup ends)
+            return;
+        }
+        const int c = D + 1;
+        int err = (c + 1 > P) ? kErrPool : 0;
+        if (value_lim(1, omr) != 1) err |= kErrValueSet;
+        if (SEL && Ds + 1 > PS) err |= kErrPath;
+        if (SEL && !err && root_vis0 >= PS) err |= kErrTable;  // the root's child visits index the pUCT table
+        const bool wild_any = ballot(l < A && !tame_prior(pol * 1.0f / bet)) != 0;
+        const bool pred_fast = !SEL || (fast_ok && htame && !wild_any && tame_val(v_in) && tame_val(r_in) &&
+                                        fabsf(discount) <= 1.0f);
+        if (l == 0) sXi[2] = pred_fast ? 1 : 0;
+        stamp(ts, 2);
+        lds_barrier();
+        stamp(ts, 3);
+        if (pred_fast && l < kNxt) hp->nxt[l] = (wi >= 0 && wi < gW) ? w_raw : 0u;
+        stamp(ts, 4);
+        if (SEL && ROW != 3 && !err) {
+            char *dst = gather_out + (long long)t * row_bytes;
+            if constexpr (ROW == 1) {
+                if (o < row_bytes) *(int4 *)(dst + o) = gv0;
+                if (o + 1024 < row_bytes) *(int4 *)(dst + o + 1024) = gv1;
+                if (o + 2048 < row_bytes) *(int4 *)(dst + o + 2048) = gv2;
+                if (o + 3072 < row_bytes) *(int4 *)(dst + o + 3072) = gv3;
+            } else if constexpr (ROW == 2) {
+                wait_vm();
+                for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(dst + o2) = *(const int4 *)(sbig + o2);
+            } else {  // any other row: 16-byte copies when aligned, else 4-byte
+                if (((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) & 15) == 0) {
+                    for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(dst + o2) = *(const int4 *)(src + o2);
+                } else {
+                    for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
+                        *(int *)(dst + o2) = *(const int *)(src + o2);
+                }
+            }
+        }
+        stamp(ts, 5);
+        if (MZ_STAMPS && l == 0) {  // (wave 2's phases, stamped builds: slots wave 0 leaves alone)
+            st[MZ_S_CYC_STAGE1] += (long long)(ts[1] - ts[0]);  // scalar round trip
+            st[MZ_S_CYC_STAGE2] += (long long)(ts[2] - ts[0]);  // arrival at the barrier
+            st[MZ_S_CYC_GATHER] += (long long)(ts[4] - ts[0]);  // engine words landed (after the barrier)
+            st[MZ_S_CYC_W1_STAGE2] += (long long)(ts[5] - ts[0]);  // row stored
+        }
+        if (l < MZ_S_CYC_HEADER) {
+            long long add = 0;
+            switch (l) {
+                case MZ_S_SELECTS: add = SEL ? 1 : 0; break;
+                case MZ_S_PATH_EDGES: add = SEL ? Ds : 0; break;
+                case MZ_S_SCORED: add = SEL ? Ds : 0; break;
+                case MZ_S_EXPANDS: add = 1; break;
+                case MZ_S_NEW_CHILDREN: add = 1; break;
+                case MZ_S_BACKUP_NODES: add = D + 1; break;
+                case MZ_S_MINMAX_NODES: add = D; break;
+                default: break;
+            }
+            st[l] = st_old + add;
+        }
+        if constexpr (ROW == 2) wait_vm();
+        span_end(hsx, 2);
+        return;
+    }
+
+    // ======== wave 0: CTree::expand (cnode.cpp:224-295) of the leaf: one draw ========
+    int16v hv = sload16(hp);  // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf, tame, nxt[0 .. 6]
+    int root_vis0 = sload1(&d.A()[nb].x);
+    int r_i = sload1(reward + t), v_i = sload1(value + t);
+    int4v lb = sload4(&d.Bn()[nb + Dp]);
+    int4v io_xy = sload4((const char *)iop + offsetof(ChainIO, idx_x));  // idx_x, idy
+    int2v io_a = sload2((const char *)iop + offsetof(ChainIO, act));
+    int omri = sload1(&pl->g.one_minus_rho);
+    const float pol = policy[(size_t)t * A + (l < A ? l : 0)];
+    const float bet = beta[(size_t)t * A + (l < A ? l : 0)];
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+s"(hv), "+s"(root_vis0), "+s"(r_i), "+s"(v_i), "+s"(lb), "+s"(io_xy), "+s"(io_a), "+s"(omri)
+                 :
+                 : "memory");
+    const float r_in = i2f(r_i), v_in = i2f(v_i);
+    int *const idx_x = (int *)(gchar *)u64_of(io_xy[0], io_xy[1]), *const idy = (int *)(gchar *)u64_of(io_xy[2], io_xy[3]);
+    int *const act = (int *)(gchar *)u64_of(io_a[0], io_a[1]);
+    int4 leaf_b = make_int4(lb.x, lb.y, lb.z, lb.w);
+    TreeHdr h;
+    h.cursor = hv[0];
+    h.tot = hv[1];
+    h.D = hv[2];
+    h.err = hv[3];
+    h.leaf = hv[7];
+    h.tame = hv[8];
+    h.nxt[0] = (unsigned)hv[9];
+    h.nxt[1] = (unsigned)hv[10];
+    d.o_err = pl->d.o_err;
+    if (h.err) {  // a dead tree stays dead and re-reports its error
+        if (l == 0) {
+            if (SEL) {
+                idx_x[t] = 0;
+                idy[t] = t;
+                act[t] = 0;
+            }
+            atomicOr(d.err(), h.err);
+        }
+        return;
+    }
+    const int D = h.D;
+    if (D != Dp || h.tot != D + 1 || h.leaf != D) {
+        if (D + 1 > P || h.tot != D + 1 || h.leaf != D) {  // not a chain: refuse
+            if (l == 0) {
+                if (SEL) {
+                    idx_x[t] = 0;
+                    idy[t] = t;
+                    act[t] = 0;
+                }
+                hp->err = kErrPath;
+                atomicOr(d.err(), kErrPath);
+            }
+            return;
+        }
+        leaf_b = d.Bn()[nb + D];  // out of sequence: the header's leaf
+    }
+    stamp(ts, 1);
+    int err = 0;
+    const int leaf = D, c = D + 1;  // the new child
+    int cursor = h.cursor;
+    int a = 0;
+    if (A >= 2) {
+        const double cp = cdf_bcast(bet, A, (float *)(smem + L.oW), (double *)(smem + L.oP));
+        const double w1 = (double)h.nxt[0], w2 = (double)h.nxt[1];
+        double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
+        if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+        a = __popcll(ballot(l < A && cp < u));    // lower_bound
+        cursor += 2;
+    }
+    a = uni(a);
+    stamp(ts, 2);
+    const float omr = i2f(omri);
+    if (c + 1 > P) err |= kErrPool;
+    if (value_lim(1, omr) != 1) err |= kErrValueSet;  // (count 1: size_lim must be 1, utils.cpp:31)
+    const float bh = 1.0f;  // betahat_prob = count / sampled_times = 1 / 1
+    const float pol_a = rlf(pol, a), bet_a = rlf(bet, a);
+    const float prior = pol_a * bh / bet_a;  // prior * betahat_prob / beta_prob (eps = 0 after the root)
+    const bool wild = !tame_prior(prior);
+    leaf_b = uni4(leaf_b);
+    if (!err && l == 0) {
+        const size_t gi = nb + c;
+        d.A()[gi] = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+        d.Bn()[gi] = make_int4(0, pack_y(0, a, -1), f2i(0.0f), -1);
+        d.C()[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d.PP()[gi] = v_in;
+        if (leaf == 0) {  // (readbacks: root children)
+            d.o_D = pl->d.o_D;
+            d.D()[gi] = make_float4(pol_a, bet_a, bh, 0.f);
+        }
+        const int md = md_of(leaf_b.y) < 0 ? 0 : md_of(leaf_b.y);
+        d.Bn()[nb + leaf] = make_int4(c, pack_y(1, act_of(leaf_b.y), md), f2i(v_in), hsx);
+    }
+    const int tame = (h.tame && !wild && tame_val(v_in) && tame_val(r_in)) ? 1 : 0;
+    const bool fast = !SEL || (fast_ok && tame && fabsf(discount) <= 1.0f);  // (no selection: no words)
+    const int Ds = c;
+    if (SEL && Ds + 1 > PS) err |= kErrPath;
+    // the root's total child visits after this back-propagation index the pUCT table (select_walk
+    // checks it in the fast case; in the exact case it is the largest parent count of the path)
+    if (SEL && root_vis0 >= PS && (fast || !err)) err |= kErrTable;
+    if (SEL && l == 0) {
+        idx_x[t] = err ? 0 : hsx;  // parent->hidden_state_index_x: the expanded leaf's
+        idy[t] = t;
+        act[t] = err ? 0 : a;
+    }
+    stamp(ts, 3);
+    lds_barrier();  // wave 1's back-propagation (sA, sPP) and min / max; wave 2's flag
+    stamp(ts, 4);
+    const float mn = unif(sX[0]), mx = unif(sX[1]);
+    const bool w2_words = sXi[2] != 0;
+    const int mm_cnt = D;
+    int words = 0;
+    if (SEL && fast) {
+        words = Ds - ((root_vis0 + 1 <= 1) ? 1 : 0);  // one per level but the forced first one
+    } else if (SEL && !err) {
+        // ---- select_walk's exact case: every level's tie list must be non-empty to consume a
+        // word (score >= FLOAT_MIN, not NaN); levels 1..Ds scored in parallel ----
+        sA[c] = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+        wait_lds();
+        const int root_visit = uni(sA[0].x);
+        const float gdelta = pl->g.delta;
+        const bool mm_on = mm_cnt > 0;
+        float den = 0.f;
+        if (mm_on) {
+            const float delta = mx - mn;
+            den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
+        }
+        d.o_pb = pl->d.o_pb;
+        d.o_sq = pl->d.o_sq;
+        const float *pbt = d.pb();
+        const double *sqt = d.sq();
+        for (int i0 = 0; i0 <= Ds; i0 += kWave) {
+            const int i = i0 + l;
+            bool valid = false;
+            if (i >= 1 && i <= Ds && !(i == 1 && root_visit <= 1)) {
+                const int n = sA[i - 1].x - 1;  // the parent's total_children_visit_counts (< PS: checked)
+                const int4 ca = sA[i];
+                const float pp = (i == Ds) ? v_in : sPP[i];
+                float vs = (ca.x == 0) ? 0.0f : ((i2f(ca.w) + discount * i2f(ca.z)) - pp);
+                if (mm_on) vs = (vs - mn) / den;
+                if (vs < 0) vs = 0;
+                if (vs > 1) vs = 1;
+                const float pbc = (float)((double)pbt[n] * (sqt[n] / (double)(ca.x + 1)));
+                const float sc = pbc * i2f(ca.y) + vs;
+                valid = sc >= -1000000.0f;  // FLOAT_MIN (utils.h:12)
+            }
+            words += __popcll(ballot(valid));
+        }
+    }
+    stamp(ts, 5);
+    if (!w2_words && l < kNxt) {  // (wave 2 wrote them when the fast case was certain)
+        const int gW = pl->g.W;
+        const unsigned *Rt = (const unsigned *)(base + (size_t)pl->d.o_R * 256) + (size_t)t * gW;
+        unsigned nxt_w = 0;
+        if ((fast || (SEL && !err)) && cursor + words + l < gW) nxt_w = Rt[cursor + words + l];
+        hp->nxt[l] = nxt_w;
+    }
+    if (l == 0) {
+        hp->cursor = err ? h.cursor : cursor + words;
+        hp->tot = err ? h.tot : c + 1;
+        hp->D = (err || !SEL) ? h.D : Ds;
+        hp->err = err;
+        hp->mm_min = mn;
+        hp->mm_max = mx;
+        hp->mm_cnt = mm_cnt;
+        hp->tame = tame;
+        hp->leaf = (err || !SEL) ? h.leaf : c;
+    }
+    stamp(ts, 6);
+    if (MZ_STAMPS && l >= MZ_S_CYC_HEADER && l < MZ_S_COUNT) {
+        d.o_stats = pl->d.o_stats;
+        long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
+        long long add = 0;
+        switch (l) {
+            case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;   // round 1
+            case MZ_S_CYC_EXP_CDF: add = (long long)(ts[2] - ts[1]); break;  // distribution + draw
+            case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;   // child, outputs
+            case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;   // waiting at the barrier
+            case MZ_S_CYC_SELECT: add = (long long)(ts[5] - ts[4]); break;   // selection (exact case)
+            case MZ_S_CYC_EPILOGUE: add = (long long)(ts[6] - ts[5]); break; // header
+            case MZ_S_CYC_BAK_BOOT: add = sXl[0]; break;                     // wave 1: recurrence
+            case MZ_S_CYC_BAK_NODES: add = sXl[1]; break;                    // wave 1: node updates
+            case MZ_S_CYC_W1_ROUND1: add = sXl[2]; break;                    // wave 1: round 1
+            case MZ_S_STAMPED: add = 1; break;
+            default: break;
+        }
+        const bool w2_slot = l == MZ_S_CYC_STAGE1 || l == MZ_S_CYC_STAGE2 || l == MZ_S_CYC_GATHER ||
+                             l == MZ_S_CYC_W1_STAGE2;
+        if (!w2_slot) st[l] += add;
+    }
+    if (l == 0 && err) atomicOr(d.err(), err);
+    span_close(hsx, rt0);
+}
+
+// ================================================================================================
 // General trees (2 <= sampled_times <= 64, agent_num = 1, pools of <= 1024 nodes): the fused
 // simulation step on four waves
 // ================================================================================================
@@ -4253,6 +4854,7 @@ struct mz_batch {
     long long expansions = 0;  // expansions since prepare (incl. the root's): bounds tot and depth
     int nc = 0;                // k_step layout class (0 = layout from Geo)
     int chain_nc = -1;         // k_chain node class for K = 1 trees (-1: k_step for every launch)
+    int chain3_nc = 0;         // k_chain3 node class (64 .. 1024) for K = 1 trees, 0: k_chain / k_step
     int tree_nc = -1;          // k_tree node class for 2 <= K <= 64 trees (-1: k_step)
     Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
 };
@@ -4414,6 +5016,37 @@ void launch_chain(mz_batch *b, const StepArgs &a, int lds) {
                        a.reward, a.value, a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act);
 }
 
+template <int NC, bool SEL, int ROW>
+void launch_chain3_row(mz_batch *b, const StepArgs &a) {
+    const Geo &g = b->geo;
+    const Dev &dv = b->dev;
+    // (the first 14 argument dwords, through the discount, arrive preloaded in SGPRs)
+    const ChainIO io{a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act};
+    hipLaunchKernelGGL((k_chain3<NC, SEL, ROW>), dim3(g.B), dim3(3 * kWave),
+                       chain3_lds_bytes(NC) + (ROW == 2 ? 16 * 16 * kWave : 0), b->stream, (char *)dv.base, a.policy,
+                       a.beta, a.reward, a.value, g.P | (g.PS << 16),
+                       (int)((unsigned)g.B | ((unsigned)g.A << 24) | ((unsigned)b->fast_ok << 31)), a.hsx, a.discount,
+                       io);
+}
+// the row class of a launch (k_chain3's ROW)
+int chain3_row(const StepArgs &a, bool sel) {
+    if (!sel || !a.pool) return 3;
+    const bool al = ((a.row_bytes | a.pool_stride | (long long)(uintptr_t)a.pool | (long long)(uintptr_t)a.gather_out) &
+                     15) == 0;
+    if (al && a.row_bytes > 0 && a.row_bytes <= 4 * 16 * kWave) return 1;
+    if (al && a.row_bytes > 0 && a.row_bytes <= 16 * 16 * kWave) return 2;
+    return 0;
+}
+template <int NC, bool SEL = true>
+void launch_chain3(mz_batch *b, const StepArgs &a) {
+    switch (chain3_row(a, SEL)) {
+        case 1: launch_chain3_row<NC, SEL, 1>(b, a); break;
+        case 2: launch_chain3_row<NC, SEL, 2>(b, a); break;
+        case 3: launch_chain3_row<NC, SEL, 3>(b, a); break;
+        default: launch_chain3_row<NC, SEL, 0>(b, a); break;
+    }
+}
+
 template <int NC, bool SEL = true>
 void launch_tree(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
@@ -4425,6 +5058,25 @@ void launch_tree(mz_batch *b, const StepArgs &a) {
 
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
+    if (eb && b->chain3_nc > 0) {  // K = 1 trees: the three-wave chain kernel
+        if (sel) {
+            switch (b->chain3_nc) {
+                case 64: launch_chain3<64>(b, a); break;
+                case 128: launch_chain3<128>(b, a); break;
+                default: launch_chain3<256>(b, a); break;
+            }
+        } else {
+            switch (b->chain3_nc) {
+                case 64: launch_chain3<64, false>(b, a); break;
+                case 128: launch_chain3<128, false>(b, a); break;
+                default: launch_chain3<256, false>(b, a); break;
+            }
+        }
+        HIP_TRY(hipGetLastError());
+        b->rb_valid = b->rb_dev_valid = false;
+        ++b->expansions;
+        return MZ_OK;
+    }
     if (eb && b->chain_nc >= 0) {  // K = 1 trees: the chain kernel
         const bool big = sel && a.pool && a.row_bytes > 4 * 16 * kWave && a.row_bytes <= 16 * 16 * kWave;
         const int lds = chain_lds_bytes(g.P, b->chain_nc) + (big ? 16 * 16 * kWave : 0);
@@ -4721,6 +5373,12 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     {
         ArenaPlan plan;
         plan.ptr(&b->prm, 1);
+        plan.dev<int4>(d.o_A, nodes);
+        plan.dev<int>(d.o_Par, nodes);
+        plan.dev<int4>(d.o_Bn, nodes);
+        plan.dev<float>(d.o_Q, nodes);
+        plan.dev<float>(d.o_PP, nodes);
+        plan.dev<float4>(d.o_C, nodes);
         plan.dev<TreeHdr>(d.o_hdr, (size_t)B);
         plan.dev<long long>(d.o_stats, (size_t)B * MZ_S_COUNT);
         plan.dev<int>(d.o_err, 1);
@@ -4729,12 +5387,6 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         plan.dev<float>(d.o_T, (size_t)g.TT + 4 * kWave);
         plan.dev<float>(d.o_pb, (size_t)b->PS + kWave);
         plan.dev<double>(d.o_sq, (size_t)b->PS + kWave);
-        plan.dev<int4>(d.o_A, nodes);
-        plan.dev<int>(d.o_Par, nodes);
-        plan.dev<int4>(d.o_Bn, nodes);
-        plan.dev<float>(d.o_Q, nodes);
-        plan.dev<float>(d.o_PP, nodes);
-        plan.dev<float4>(d.o_C, nodes);
         plan.dev<int2>(d.o_path, (size_t)B * b->PS);
         plan.dev<int2>(d.o_V, nodes * b->E);
         plan.dev<unsigned>(d.o_R, (size_t)B * b->W);
@@ -4762,6 +5414,10 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         mz_destroy(b);
         return fail(MZ_ERR_DEVICE, m);
     }
+    // k_chain3 takes P and PS in 16 bits each (K = 1 pools of <= 1024 nodes always fit)
+    // (pools above 256 nodes keep k_chain: wave 1 holds the chain's records in registers, 8 per 64 nodes)
+    if (b->chain_nc > 0 && b->chain_nc <= 256 && b->P < 65536 && b->PS < 65536 && !getenv_flag("MZ_CHAIN_V2"))
+        b->chain3_nc = b->chain_nc;
     const Params host_params{b->geo, b->dev};
     std::vector<float> lp(b->PS + 1 + kWave, 0.f);
     lp[0] = 1.0f;
@@ -5216,10 +5872,10 @@ int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *ou
 
 #if MZ_SPANS
 // diagnostic builds only (not in include/mzmcts.h): reset == 1 zeroes the launch spans; else
-// out[(k * trees + t) * 2 + {0, 1}] = slot k's tree t start / end (100 MHz ticks; 0 = no launch),
-// k < slots <= 256, t < trees <= 1024
+// out[((k * trees + t) * 4 + {0, 1, 2, 3}] = slot k's tree t: wave 0 start, wave 0 end, wave 1 end,
+// wave 2 end (100 MHz ticks; 0 = no such launch / wave), k < slots <= 256, t < trees <= 1024
 int mz_debug_spans(unsigned long long *out, int slots, int trees, int reset) {
-    static ulonglong2 host[kSpanSlots][kSpanTrees];
+    static ulonglong2 host[kSpanSlots][kSpanTrees][2];
     HIP_TRY(hipDeviceSynchronize());
     if (reset) {
         std::memset(host, 0, sizeof(host));
@@ -5230,8 +5886,11 @@ int mz_debug_spans(unsigned long long *out, int slots, int trees, int reset) {
     HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_span), sizeof(host)));
     for (int k = 0; k < slots; ++k)
         for (int t = 0; t < trees; ++t) {
-            out[((size_t)k * trees + t) * 2] = host[k][t].x;
-            out[((size_t)k * trees + t) * 2 + 1] = host[k][t].y;
+            unsigned long long *o = out + ((size_t)k * trees + t) * 4;
+            o[0] = host[k][t][0].x;
+            o[1] = host[k][t][0].y;
+            o[2] = host[k][t][1].x;
+            o[3] = host[k][t][1].y;
         }
     return MZ_OK;
 }
