@@ -2459,51 +2459,6 @@ __device__ __forceinline__ ChainLayout<NC> chain_layout(int P) {
 }
 int chain_lds_bytes(int P, int nc) { return ChainLayout<0>(nc > 0 ? nc : P).total; }
 
-// std::discrete_distribution's cumulative table (libstdc++ random.tcc:2656-2690, as cdf_lane) for
-// the weights bet (lane a < A): the sequential double sum and the sequential prefix sums run on
-// every lane from broadcast LDS reads (16 operands per batch of four 16-byte reads) instead of
-// v_readlane.  Trailing +0.0 terms of a batch are exact no-ops on the non-negative sums.  Lane a
-// returns cp[a] (cp[A-1] forced to 1.0).
-__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp) {
-    const int l = lane_id();
-    sw[l] = (l < A) ? bet : 0.f;  // kMaxActions = kWave entries
-    wait_lds();
-    double sum = 0.0;
-    for (int a0 = 0; a0 < A; a0 += 16) {
-        float w[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 v = *(const float4 *)(sw + a0 + 4 * q);
-            w[4 * q] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sum += (double)w[j];
-    }
-    const double p = (l < A) ? (double)bet / sum : 0.0;
-    sp[l] = p;
-    wait_lds();
-    double acc = 0.0, cp = 0.0;
-    for (int a0 = 0; a0 < A; a0 += 16) {
-        double pj[16];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
-            pj[2 * q] = v.x;
-            pj[2 * q + 1] = v.y;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            acc = (a0 + j == 0) ? pj[0] : acc + pj[j];
-            cp = sel_lane(cp, acc, 1ull << (j & 63) << (a0 & 63));
-        }
-    }
-    if (l == A - 1) cp = 1.0;
-    return cp;
-}
-
 // n dwords global -> LDS by LDS-DMA (asm, uncounted by the compiler): 16-byte chunks when src and dst
 // are 16-byte aligned (a quarter of the instructions; up to 3 dwords past n are read and written:
 // callers' arrays are padded), else dwords
@@ -2531,8 +2486,48 @@ __device__ __forceinline__ float ldsc(const float *p) {
     return *(const __attribute__((address_space(4))) float *)p;
 }
 
-// cdf_bcast for weights already staged in sw[0..A) (sw[l] = 0 for l >= A)
-__device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp) {
+// std::discrete_distribution's cumulative table (libstdc++ random.tcc:2656-2690, as cdf_lane) for
+// the weights staged in sw[0 .. 64) (sw[l] = 0 for l >= A; lane l's own weight is wl): the
+// sequential double sum and the sequential prefix sums run on every lane from broadcast LDS reads
+// instead of v_readlane.  N terms (A <= N): trailing +0.0 terms are exact no-ops on the
+// non-negative sums, so N only has to cover A -- the class (4, 8, 12, 16) is picked once per call,
+// not per term.  Lane a returns cp[a] (cp[A-1] forced to 1.0).
+template <int N>
+__device__ __forceinline__ double cdf_terms(int A, const float *sw, double *sp, float wl) {
+    const int l = lane_id();
+    float w[N];
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+        const float4 v = *(const float4 *)(sw + 4 * q);
+        w[4 * q] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) sum += (double)w[j];
+    const double p = (l < A) ? (double)wl / sum : 0.0;
+    sp[l] = p;
+    wait_lds();
+    double pj[N];
+#pragma unroll
+    for (int q = 0; q < N / 2; ++q) {
+        const double2 v = *(const double2 *)(sp + 2 * q);
+        pj[2 * q] = v.x;
+        pj[2 * q + 1] = v.y;
+    }
+    double acc = pj[0], cp = (l == 0) ? pj[0] : 0.0;
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        acc = acc + pj[j];
+        cp = sel_lane(cp, acc, 1ull << j);
+    }
+    if (l == A - 1) cp = 1.0;
+    return cp;
+}
+// A > 16: batches of 16 terms
+__device__ __forceinline__ double cdf_long(int A, const float *sw, double *sp, float wl) {
     const int l = lane_id();
     double sum = 0.0;
     for (int a0 = 0; a0 < A; a0 += 16) {
@@ -2548,7 +2543,7 @@ __device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp)
 #pragma unroll
         for (int j = 0; j < 16; ++j) sum += (double)w[j];
     }
-    const double p = (l < A) ? (double)sw[l] / sum : 0.0;
+    const double p = (l < A) ? (double)wl / sum : 0.0;
     sp[l] = p;
     wait_lds();
     double acc = 0.0, cp = 0.0;
@@ -2568,6 +2563,26 @@ __device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp)
     }
     if (l == A - 1) cp = 1.0;
     return cp;
+}
+// cdf for weights already staged in sw[0..A) (sw[l] = 0 for l >= A)
+__device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp) {
+    const float wl = sw[lane_id()];
+    if (A <= 4) return cdf_terms<4>(A, sw, sp, wl);
+    if (A <= 8) return cdf_terms<8>(A, sw, sp, wl);
+    if (A <= 12) return cdf_terms<12>(A, sw, sp, wl);
+    if (A <= 16) return cdf_terms<16>(A, sw, sp, wl);
+    return cdf_long(A, sw, sp, wl);
+}
+// the same for the weights bet held one per lane (lane a < A)
+__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp) {
+    const int l = lane_id();
+    sw[l] = (l < A) ? bet : 0.f;  // kMaxActions = kWave entries
+    wait_lds();
+    if (A <= 4) return cdf_terms<4>(A, sw, sp, bet);
+    if (A <= 8) return cdf_terms<8>(A, sw, sp, bet);
+    if (A <= 12) return cdf_terms<12>(A, sw, sp, bet);
+    if (A <= 16) return cdf_terms<16>(A, sw, sp, bet);
+    return cdf_long(A, sw, sp, bet);
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
@@ -3232,31 +3247,22 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
     }
 
     if (wv == 2) {
-        // ======== wave 2: the leaf-row gather, the next expansion's engine words, the counters ========
+        // ======== wave 2: the leaf-row gather and the counters ========
         // Straight-line code in issue order (the row class ROW is a template argument): every wait
         // the compiler places then counts exactly the loads issued after the one it needs.
-        const float pol = policy[(size_t)t * A + (l < A ? l : 0)];
-        const float bet = beta[(size_t)t * A + (l < A ? l : 0)];
         // (one scalar round trip: the outputs' kernel arguments, the header, the handle's constants)
         int8v io8 = sload8((const void *)iop);  // pool, pool_stride, row_bytes, gather_out
-        int16v hv = sload16(hp);                // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf, tame, ...
-        int rv0 = sload1(&d.A()[nb].x), r_i = sload1(reward + t), v_i = sload1(value + t);
-        int gWi = sload1(&pl->g.W), omri = sload1(&pl->g.one_minus_rho), oRi = sload1(&pl->d.o_R);
-        int osti = sload1(&pl->d.o_stats);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+s"(io8), "+s"(hv), "+s"(rv0), "+s"(r_i), "+s"(v_i), "+s"(gWi), "+s"(omri), "+s"(oRi), "+s"(osti)
-                     :
-                     : "memory");
+        int8v hv = sload8(hp);                  // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf
+        int rv0 = sload1(&d.A()[nb].x), omri = sload1(&pl->g.one_minus_rho), osti = sload1(&pl->d.o_stats);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(io8), "+s"(hv), "+s"(rv0), "+s"(omri), "+s"(osti) : : "memory");
         stamp(ts, 1);
         // (typed as global memory: flat accesses would count against lgkmcnt too)
         const char *pool = (const char *)(const gchar *)u64_of(io8[0], io8[1]);
         const long long pool_stride = (long long)u64_of(io8[2], io8[3]);
         const long long row_bytes = (long long)u64_of(io8[4], io8[5]);
         char *gather_out = (char *)(gchar *)u64_of(io8[6], io8[7]);
-        const int cur0 = hv[0], toth = hv[1], D = hv[2], herr = hv[3], leafh = hv[7], htame = hv[8];
+        const int toth = hv[1], D = hv[2], herr = hv[3], leafh = hv[7];
         const int root_vis0 = rv0;
-        const float r_in = i2f(r_i), v_in = i2f(v_i);
-        const int gW = gWi;
         const float omr = i2f(omri);
         // the row of this launch's leaf (hidden_state_index_x = hsx), issued first
         const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
@@ -3275,33 +3281,20 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         d.o_stats = (unsigned)osti;
         long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
         const long long st_old = st[l < MZ_S_CYC_HEADER ? l : 0];
-        // the engine words after this launch's draw and selection, when select_walk's fast case is
-        // certain (every prior the expansion can create tame: whatever the draw); clamped addresses
-        const int Ds = D + 1;
-        const int words = SEL ? Ds - ((root_vis0 + 1 <= 1) ? 1 : 0) : 0;
-        const int cur = cur0 + ((A >= 2) ? 2 : 0) + words;
-        const unsigned *Rt = (const unsigned *)(base + (size_t)(unsigned)oRi * 256) + (size_t)t * gW;
-        const int wi = cur + l;
-        const unsigned w_raw = Rt[(wi >= 0 && wi < gW) ? wi : 0];
         // a dead or inconsistent tree: wave 0 reports; no wave takes the barrier on these paths (all
         // three read the same header)
         if (herr || D + 1 > P || toth != D + 1 || leafh != D) {
             wait_vm();  // (no LDS-DMA may land after the workgroup ends)
             return;
         }
-        const int c = D + 1;
+        const int c = D + 1, Ds = c;
         int err = (c + 1 > P) ? kErrPool : 0;
         if (value_lim(1, omr) != 1) err |= kErrValueSet;
         if (SEL && Ds + 1 > PS) err |= kErrPath;
         if (SEL && !err && root_vis0 >= PS) err |= kErrTable;  // the root's child visits index the pUCT table
-        const bool wild_any = ballot(l < A && !tame_prior(pol * 1.0f / bet)) != 0;
-        const bool pred_fast = !SEL || (fast_ok && htame && !wild_any && tame_val(v_in) && tame_val(r_in) &&
-                                        fabsf(discount) <= 1.0f);
-        if (l == 0) sXi[2] = pred_fast ? 1 : 0;
         stamp(ts, 2);
-        lds_barrier();
+        lds_barrier();  // (early: waves 0 and 1 must not wait for this wave's row)
         stamp(ts, 3);
-        if (pred_fast && l < kNxt) hp->nxt[l] = (wi >= 0 && wi < gW) ? w_raw : 0u;
         stamp(ts, 4);
         if (SEL && ROW != 3 && !err) {
             char *dst = gather_out + (long long)t * row_bytes;
@@ -3355,13 +3348,23 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
     int4v lb = sload4(&d.Bn()[nb + Dp]);
     int4v io_xy = sload4((const char *)iop + offsetof(ChainIO, idx_x));  // idx_x, idy
     int2v io_a = sload2((const char *)iop + offsetof(ChainIO, act));
-    int omri = sload1(&pl->g.one_minus_rho);
+    int omri = sload1(&pl->g.one_minus_rho), gWi = sload1(&pl->g.W), oRi = sload1(&pl->d.o_R);
     const float pol = policy[(size_t)t * A + (l < A ? l : 0)];
     const float bet = beta[(size_t)t * A + (l < A ? l : 0)];
     asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+s"(hv), "+s"(root_vis0), "+s"(r_i), "+s"(v_i), "+s"(lb), "+s"(io_xy), "+s"(io_a), "+s"(omri)
+                 : "+s"(hv), "+s"(root_vis0), "+s"(r_i), "+s"(v_i), "+s"(lb), "+s"(io_xy), "+s"(io_a), "+s"(omri),
+                   "+s"(gWi), "+s"(oRi)
                  :
                  : "memory");
+    // The next expansion's engine words (the header's nxt), read now for select_walk's fast case --
+    // one word per level below the root (its first level is forced while it has one visit): they
+    // land while the distribution is built.  The exact case re-reads them after the barrier.
+    const int gW = gWi;
+    const unsigned *Rt = (const unsigned *)(base + (size_t)(unsigned)oRi * 256) + (size_t)t * gW;
+    const int dA = (A >= 2) ? 2 : 0;
+    const int words_fast = SEL ? (hv[2] + 1) - ((root_vis0 + 1 <= 1) ? 1 : 0) : 0;
+    const int wi = hv[0] + dA + words_fast + l;
+    const unsigned w_fast = Rt[(wi >= 0 && wi < gW) ? wi : 0];
     const float r_in = i2f(r_i), v_in = i2f(v_i);
     int *const idx_x = (int *)(gchar *)u64_of(io_xy[0], io_xy[1]), *const idy = (int *)(gchar *)u64_of(io_xy[2], io_xy[3]);
     int *const act = (int *)(gchar *)u64_of(io_a[0], io_a[1]);
@@ -3455,7 +3458,6 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
     lds_barrier();  // wave 1's back-propagation (sA, sPP) and min / max; wave 2's flag
     stamp(ts, 4);
     const float mn = unif(sX[0]), mx = unif(sX[1]);
-    const bool w2_words = sXi[2] != 0;
     const int mm_cnt = D;
     int words = 0;
     if (SEL && fast) {
@@ -3496,11 +3498,13 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         }
     }
     stamp(ts, 5);
-    if (!w2_words && l < kNxt) {  // (wave 2 wrote them when the fast case was certain)
-        const int gW = pl->g.W;
-        const unsigned *Rt = (const unsigned *)(base + (size_t)pl->d.o_R * 256) + (size_t)t * gW;
+    if (l < kNxt) {
         unsigned nxt_w = 0;
-        if ((fast || (SEL && !err)) && cursor + words + l < gW) nxt_w = Rt[cursor + words + l];
+        if (fast) {
+            nxt_w = (wi >= 0 && wi < gW) ? w_fast : 0u;  // (cursor + words + l == wi)
+        } else if (SEL && !err && cursor + words + l < gW) {
+            nxt_w = Rt[cursor + words + l];
+        }
         hp->nxt[l] = nxt_w;
     }
     if (l == 0) {

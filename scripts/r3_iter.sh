@@ -1,13 +1,13 @@
 #!/bin/bash
 # Chain-kernel iteration pass (one GPU box): GPU tests, then the headline-style bench of the new
 # k_chain3 against k_chain (MZ_CHAIN_V2=1) at the K = 1 BASELINE configurations, the stamped build
-# and the spans build.  STEPS selects: pytest ab stamps spans.  A fault / abort / timeout ends it.
+# and the spans build.  STEPS selects: pytest ab ktree stamps spans.  A fault / abort / timeout ends it.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$(pwd)
 export TMPDIR=/tmp
 O=gpurun_out/it
 mkdir -p $O
-STEPS=${STEPS:-"pytest ab stamps spans"}
+STEPS=${STEPS:-"pytest ab ktree stamps spans"}
 summ() { python - "$@" <<'PY'
 import json, sys
 for f in sys.argv[1:]:
@@ -38,6 +38,12 @@ for s in $STEPS; do
                 MZ_CHAIN_V2=1 run ab_${n}_v2 300 $a
             done
             summ $O/ab_*.json ;;
+    ktree)  for cfg in "3m_k5:--map 3m --sampled-times 5" "3s5z_k5:--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5" \
+                       "27m_k5:--map 27m_vs_30m --sims 200 --sampled-times 5"; do
+                n=${cfg%%:*}; a=${cfg#*:}
+                run kt_${n} 300 $a
+            done
+            summ $O/kt_*.json ;;
     stamps) MZ_STAMPS=1 run stamps_3m 200; summ $O/stamps_3m.json ;;
     spans)  MZ_LIB_OVERRIDE=$R/mazero_amd/_build/variant_spans.so run spans_3m 200
             MZ_LIB_OVERRIDE=$R/mazero_amd/_build/variant_spans.so MZ_CHAIN_V2=1 run spans_3m_v2 200
