@@ -8,7 +8,8 @@ roots, i.e. 38,400 root-simulations per step per GPU.
 Per search the device executes exactly what mazero_amd.mcts_sampled runs around the network:
   k_prepare (RNG stream + root expansion + the selection of simulation 0)
   49 x fused <expand+backup, select, gather>  ->  1 x <expand+backup>  ->  one k_readback
-where the fused kernel is k_chain (K = 1), k_tree (2 <= K <= 64, pools <= 1024 nodes) or k_step
+where the fused kernel is k_chain3 (K = 1, pools <= 256 nodes), k_chain (K = 1, larger pools), k_tree
+(2 <= K <= 64, pools <= 1024 nodes) or k_step
 (fused_kernel_name below)
 with the network replaced by synthetic device-resident outputs (softmax(N(0,1))
 policy = beta, reward 0.1*N(0,1), value N(0,1), Dirichlet(0.3) root noise, hidden-state pool
@@ -81,6 +82,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-procs", type=int, default=16,
                     help="processes of the multi-core CPU baseline (at most this process's CPU share)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dropin", action="store_true",
+                    help="time the tree-level drop-in instead: the reference driver's host loop "
+                         "(mcts_sampled.py:114-172, numpy in and out of every Tree_batch call) on mazero_amd.cytree")
     ap.add_argument("--backend", default="hip", choices=("hip", "port"),
                     help="'port': every rank searches on the host with the CPU port over gloo -- a CPU "
                          "test of the launcher / sharding / clock plumbing only, never a measurement")
@@ -308,11 +312,59 @@ def launch_spans(spans, S, B):
 def fused_kernel_name(K: int, P: int) -> str:
     """The per-simulation fused kernel the library launches for sampled_times K and a pool of P
     nodes (launch_step in mazero_amd/csrc/mzmcts.hip)."""
+    if K == 1 and P <= 256:
+        return "k_chain3 (K = 1 chains, three waves: fused expand+backup+select+gather)"
     if K == 1:
         return "k_chain (K = 1 chains: fused expand+backup+select+gather)"
     if 2 <= K <= 64 and P <= 1024:
         return "k_tree (four waves: fused expand+backup+select+gather)"
     return "k_step<true,true> (fused expand+backup+select+gather)"
+
+
+class DropinLeg:
+    """--dropin: what the INTEGRATION.md import swap gives a user of the reference driver -- its
+    per-simulation Tree_batch calls unchanged (mcts_sampled.py:114-172: batch_selection, then
+    batch_expansion_and_backup with numpy arrays), one env step = N sequential searches with
+    prepare and the two root readbacks the CPU baseline times too, on the MI355X library through
+    the host-memory path (every call copies its inputs in and its outputs out).  A measurement of
+    the boundary, not of the kernels."""
+
+    def __init__(self, args, host_inputs, root_offset, lib):
+        from mazero_amd.synthetic import DEFAULTS
+
+        self.args, self.B, self.root_offset, self.lib = args, host_inputs[0].B, root_offset, lib
+        N, A = CONFIGS[args.map]
+        self.N, self.A, self.S, self.K = N, A, args.sims, args.sampled_times
+        self.d = DEFAULTS
+        self.host_inputs = host_inputs
+        self.graph = None
+
+    def env_step(self):
+        from mazero_amd.cytree import Tree_batch
+
+        d, S, K = self.d, self.S, self.K
+        c2, c1, g = d["pb_c_base"], d["pb_c_init"], d["discount"]
+        for inp in self.host_inputs:
+            tb = Tree_batch(self.B, 1, self.A, K, S, d["delta_lb"], inp.seed, d["rho"], d["lam"],
+                            root_offset=self.root_offset, lib=self.lib)
+            tb.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps,
+                       inp.root_noise)
+            for s in range(S):
+                tb.batch_selection(c2, c1, g)
+                tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+            tb.get_roots_values()
+            tb.get_roots_marginal_visit_count()
+
+    def prepare(self):
+        for _ in range(max(1, self.args.warmup)):
+            self.env_step()
+
+    def check(self):
+        pass
+
+    def run(self, steps):
+        for _ in range(steps):
+            self.env_step()
 
 
 class PortLeg:
@@ -429,6 +481,8 @@ def main():
         stream = torch.cuda.Stream()
 
         def make_leg(inputs, off):
+            if args.dropin:
+                return DropinLeg(args, inputs, off, lib)
             return HipLeg(args, inputs, off, lib, dev, stream)
     else:
         def make_leg(inputs, off):
@@ -456,16 +510,16 @@ def main():
                 inputs = [slice_inputs(inp, lo, hi) for inp in inputs]
         leg = make_leg(inputs, off)
         leg.prepare()
-        st0 = leg.stats() if hip and rank == 0 else None
+        st0 = leg.stats() if hip and rank == 0 and not args.dropin else None
         elapsed = timed(leg, args.steps, world, dist, sync, dev)
-        st1 = leg.stats() if hip and rank == 0 else None
+        st1 = leg.stats() if hip and rank == 0 and not args.dropin else None
         legs[kind] = dict(leg=leg, B=B, total=total, elapsed=elapsed, st0=st0, st1=st1)
 
     main_kind = order[0]
     m = legs[main_kind]
     value = m["total"] * S * N * args.steps / m["elapsed"]
     roofline = None
-    if hip and rank == 0:
+    if hip and rank == 0 and not args.dropin:
         roofline = m["leg"].roofline(m["st0"], m["st1"], args.steps)
     cpu = None
     if hip and rank == 0 and world == 1 and not args.no_cpu:
@@ -490,6 +544,9 @@ def main():
         else:
             metric = (f"MCTS simulations/sec (whole node), SMAC {args.map}, {m['total']} roots×{S} sims"
                       + (f" ({m['B']} per GPU, weak scaling)" if main_kind == "weak" and world > 1 else ""))
+        if args.dropin:
+            metric = (f"MCTS simulations/sec, tree-level drop-in (reference driver loop on mazero_amd.cytree, "
+                      f"host numpy arrays), SMAC {args.map}, {m['total']} roots×{S} sims")
         line = {
             "metric": metric,
             "value": round(value, 1),
@@ -515,7 +572,8 @@ def main():
                 "sims": S,
                 "sampled_times": K,
                 "hidden": N * 128,
-                "graph": hip and not args.no_graph,
+                "graph": hip and not args.no_graph and not args.dropin,
+                "dropin": bool(args.dropin),
                 "backend": args.backend,
                 "parallelism": f"roots sharded over {world} GPU(s), no collective on the data path",
             },
@@ -605,6 +663,21 @@ def ptree_baseline(host_inputs, B, A, K, S, N, budget_s):
                       f"{t_run:.1f} s of tree calls, pure-Python ptree (oracle/ptree.py)"}
 
 
+def physical_cores():
+    """Physical cores of the host (distinct (physical id, core id) pairs in /proc/cpuinfo), or None."""
+    try:
+        pairs, phys_id = set(), None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys_id = line.split(":", 1)[1].strip()
+                elif line.startswith("core id"):
+                    pairs.add((phys_id, line.split(":", 1)[1].strip()))
+        return len(pairs) or None
+    except OSError:
+        return None
+
+
 def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
     """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs; plus
     SURVEY §8(d)(ii): the same env steps on several host cores at once, one process per core with
@@ -671,6 +744,15 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
     multi = {"value": round(total / wall, 1), "processes": n_proc, "cores": n_proc,
              "sample": f"{total} sims in {wall:.1f} s wall: {n_proc} processes, each searching its shard of "
                        f"the {B} roots of every agent search ({kind} ctree)"}
+    # the whole host: a GPU box grants this job one GPU's share of the node's CPUs (16), so every
+    # physical core cannot be measured there; the projection scales the measured per-process rate
+    phys = physical_cores()
+    if phys:
+        multi["whole_host_projection"] = {
+            "value": round(total / wall / n_proc * phys, 1), "cores": phys,
+            "basis": f"measured rate per process at {n_proc} processes x {phys} physical cores (linear: an upper "
+                     f"bound on the reference ctree's whole-host throughput); not measured, the pool allows "
+                     f"{n_proc} CPUs per one-GPU box"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:

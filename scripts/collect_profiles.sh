@@ -15,6 +15,7 @@ for d in gpurun_out/prof/*/; do
     grep -h '^{' "$d/traced.json" > "$dst/$c/traced.json"
     cp "$d/pmc_summary.txt" "$dst/$c/pmc_summary.txt"
     cp "$d/trace/run_kernel_stats.csv" "$dst/$c/rocprof_kernel_stats.csv"
+    [ -f "$d/window.json" ] && cp "$d/window.json" "$dst/$c/rocprof_timed_window.json"
 done
 python - "$dst/roofline_reconcile.json" gpurun_out/prof/summary.json <<'PY'
 import json, os, sys

@@ -4,6 +4,7 @@
 #   traced.json        bench.py under rocprofv3 --kernel-trace --stats (its own HIP-event timing
 #                      of the fused kernel, taken under the profiler)
 #   trace/             the rocprofv3 kernel trace + stats of that run
+#   window.json        that trace cut to the timed region (scripts/trace_window.py)
 #   pmc_fetch/, pmc_write/   separate --pmc FETCH_SIZE / WRITE_SIZE passes
 # then scripts/pmc_summary.py (-> gpurun_out/pmc_latest.json) and scripts/reconcile.py
 # (-> gpurun_out/prof/summary.json).  CONFIGS="3m_k1 ..." selects a subset.
@@ -14,12 +15,14 @@ mkdir -p gpurun_out/prof
 declare -A ARGS=(
   [3m_k1]="--map 3m --roots 256 --sims 50 --sampled-times 1"
   [3m_k5]="--map 3m --roots 256 --sims 50 --sampled-times 5"
+  [3m_k10]="--map 3m --roots 256 --sims 50 --sampled-times 10"
+  [3s5z_k10]="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10"
   [2s3z_k1]="--map 2s3z --roots 1024 --sims 50 --sampled-times 1"
   [3s5z_k5]="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5"
   [27m_k1]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1"
   [27m_k5]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5"
 )
-CONFIGS=${CONFIGS:-"3m_k1 3m_k5 2s3z_k1 3s5z_k5 27m_k1 27m_k5"}
+CONFIGS=${CONFIGS:-"3m_k1 3m_k5 3m_k10 2s3z_k1 3s5z_k5 3s5z_k10 27m_k1 27m_k5"}
 # the PMC passes run first, so the bench lines carry this build's traffic (bench.py reads
 # profiles/pmc_latest.json; on the box that copy is refreshed after every configuration)
 cp profiles/pmc_latest.json gpurun_out/pmc_latest.json 2>/dev/null
@@ -48,8 +51,12 @@ for c in $CONFIGS; do
         --out gpurun_out/pmc_latest.json
     cp gpurun_out/pmc_latest.json profiles/pmc_latest.json
     step "$d/bench.json" 300 python bench.py $a $cpu
+    # (MZ_TRACE_MARKS: fill kernels just outside the timed region, so trace_window.py can cut it out)
+    export MZ_TRACE_MARKS=1
     step "$d/traced.json" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$d/trace" -o run -- \
         python3 "$R/bench.py" --no-cpu $a
+    unset MZ_TRACE_MARKS
+    python scripts/trace_window.py "$d/trace" --bench "$d/traced.json" --out "$d/window.json" > /dev/null || exit 3
     # keep the summaries: per-dispatch traces and counter dumps of the 27m workloads are > 64 MiB
     python scripts/reconcile.py gpurun_out/prof --out gpurun_out/prof/summary.json > /dev/null || exit $?
     find "$d" -name "*kernel_trace.csv" -o -name "*counter_collection.csv" | xargs -r rm -f

@@ -45,6 +45,10 @@ for s in $STEPS; do
             done
             summ $O/kt_*.json ;;
     stamps) MZ_STAMPS=1 run stamps_3m 200; summ $O/stamps_3m.json ;;
+    kspans) MZ_LIB_OVERRIDE=$R/mazero_amd/_build/variant_spans.so run kspans_3m_k5 200 --sampled-times 5
+            MZ_LIB_OVERRIDE=$R/mazero_amd/_build/variant_spans.so run kspans_3s5z_k5 300 --map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5
+            MZ_STAMPS=1 run kstamps_3m_k5 200 --sampled-times 5
+            summ $O/kspans_*.json $O/kstamps_3m_k5.json ;;
     spans)  MZ_LIB_OVERRIDE=$R/mazero_amd/_build/variant_spans.so run spans_3m 200
             MZ_LIB_OVERRIDE=$R/mazero_amd/_build/variant_spans.so MZ_CHAIN_V2=1 run spans_3m_v2 200
             summ $O/spans_3m.json $O/spans_3m_v2.json ;;

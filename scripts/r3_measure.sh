@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-3 measurement pass (one GPU box).  STEPS selects: headline strong k10 spans trace search.
+# Round-3 measurement pass (one GPU box).  STEPS selects: headline strong k10 spans trace search
+# matrix dropin pytest spansv.
 #   headline  bench.py at its defaults (3m 256x50 K=1, CPU legs included)
 #   strong    the strong-scaling proxy: one rank's env step at B = 256/G roots (G = 8, 4, 2)
 #   k10       K = 10: 3m 256x50, 3s5z_vs_3s6z 512x100
@@ -7,6 +8,9 @@
 #   trace     rocprofv3 --kernel-trace of the headline with MZ_TRACE_MARKS=1, cut to the timed
 #             region by scripts/trace_window.py
 #   search    bench_search.py (the full loop with a network)
+#   matrix    BASELINE config #1: matrix 2-agent, 8 roots x 25 sims (CPU legs: reference ctree and the
+#             pure-Python ptree)
+#   dropin    the tree-level drop-in: the reference driver's host loop on mazero_amd.cytree
 #   pytest    the GPU test suite
 #   spansv    the spans-only build (scripts/build_variant.sh spans -DMZ_SPANS=1): launch body / boundary
 #             at 3m K=1 / K=5 untraced, then 3m K=1 under rocprofv3 --kernel-trace (same build)
@@ -41,6 +45,16 @@ for s in $STEPS; do
               python scripts/trace_window.py $O/trace_3m_k1 --bench $O/traced_3m_k1.json --out $O/window_3m_k1.json > /dev/null || exit 3
               find $O/trace_3m_k1 -name "*kernel_trace.csv" -size +30M -delete ;;
     search)   step search 900 python bench_search.py ${SEARCH_ARGS} ;;
+    matrix)   step matrix_k1 300 python bench.py --map matrix --roots 8 --sims 25 --sampled-times 1 --steps 50 --cpu-seconds 4 &&
+              step matrix_k3 300 python bench.py --map matrix --roots 8 --sims 25 --sampled-times 3 --steps 50 --cpu-seconds 4 ;;
+    memset)   # the runtime defect behind round 1's graph failure: default packet capture, then off
+              timeout -k 10 200 python -u scripts/memset_graph_repro.py 600 6 > $O/memset_repro_default.log 2>&1
+              echo "memset repro (default) rc=$?"; tail -3 $O/memset_repro_default.log
+              DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 10 200 python -u scripts/memset_graph_repro.py 600 6 \
+                  > $O/memset_repro_pc0.log 2>&1
+              echo "memset repro (packet capture off) rc=$?"; tail -3 $O/memset_repro_pc0.log ;;
+    dropin)   step dropin_3m_k1 300 python bench.py --dropin --steps 5 --warmup 1 --no-cpu &&
+              step dropin_3m_k5 300 python bench.py --dropin --steps 5 --warmup 1 --no-cpu --sampled-times 5 ;;
     pytest)   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 \
                   --timeout-method thread > $O/pytest_gpu.log 2>&1
               rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc ;;
