@@ -3766,15 +3766,27 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         const int by = uni(b4.y);
         // entries of a smaller depth / the same depth / the same depth and a smaller value; none but
         // smaller depths when the node's deepest entry is above dep (stage_regions' need test)
+        // (up to 64 entries, the usual case: one register per lane, read once; the two order
+        // statistics by readlane and the tail shift from registers)
+        const bool one = nv <= kWave;
+        int2 e1 = make_int2(0x7fffffff, 0);
+        if (one && l < nv) e1 = R[l];
         int lo = nv, c = 0, pv = 0;
         if (nv > 0 && md_of(by) >= dep) {
             lo = 0;
-            for (int e0 = 0; e0 < nv; e0 += kWave) {
-                const bool on = e0 + l < nv;
-                const int2 e = on ? R[e0 + l] : make_int2(0x7fffffff, 0);
-                lo += __popcll(ballot(on && e.x < dep));
-                c += __popcll(ballot(on && e.x == dep));
-                pv += __popcll(ballot(on && e.x == dep && i2f(e.y) < key));
+            if (one) {
+                const bool on = l < nv;
+                lo = __popcll(ballot(on && e1.x < dep));
+                c = __popcll(ballot(on && e1.x == dep));
+                pv = __popcll(ballot(on && e1.x == dep && i2f(e1.y) < key));
+            } else {
+                for (int e0 = 0; e0 < nv; e0 += kWave) {
+                    const bool on = e0 + l < nv;
+                    const int2 e = on ? R[e0 + l] : make_int2(0x7fffffff, 0);
+                    lo += __popcll(ballot(on && e.x < dep));
+                    c += __popcll(ballot(on && e.x == dep));
+                    pv += __popcll(ballot(on && e.x == dep && i2f(e.y) < key));
+                }
             }
             ent_r += nv;
         }
@@ -3785,7 +3797,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
         const int nl = value_lim(c + 1, g.one_minus_rho);
         if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
-            const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
+            const float mb = one ? rlf(i2f(e1.y), lo + c - cur) : i2f(R[lo + c - cur].y);  // *big.begin()
             if (!(key < mb)) {
                 ws -= lp * mb;
                 tw -= lp;
@@ -3798,7 +3810,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
                 tw += lp;
                 ws += lp * key;
             } else {
-                const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
+                const float ms = one ? rlf(i2f(e1.y), lo + c - cur - 1) : i2f(R[lo + c - cur - 1].y);  // *(--small.end())
                 if (key > ms) {
                     tw += lp;
                     ws += lp * key;
@@ -3819,8 +3831,12 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         } else if (l == 0) {
             G[pos] = make_int2(dep, f2i(key));
         }
-        for (int e0 = pos; e0 < nv; e0 += kWave)  // the entries after the insertion point move up by one
-            if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
+        if (one) {  // the entries after the insertion point move up by one
+            if (l >= pos && l < nv) G[l + 1] = e1;
+        } else {
+            for (int e0 = pos; e0 < nv; e0 += kWave)
+                if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
+        }
         ent_w += nv - pos + 1;
         const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
         int4 a4 = a4r;
@@ -3839,6 +3855,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             if (!is_leaf && dep > md_of(by)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(by), dep), b4.z, b4.w);
             if (i >= 1) d.Q()[gi] = q;
             sAz[n] = make_float2(val, i2f(a4.w));
+            if (i >= 1 && s.Q) s.Q[n] = q;  // the staged copy too (k_tree's scores; its min/max skips path nodes)
         }
         if (i >= 1) {
             pmn = fminf(pmn, q);
@@ -3875,15 +3892,16 @@ constexpr bool kTreeLevels = (NC >= 1024);
 // (an exact record with two or more members) takes the engine word at the cursor from the LDS
 // window (one more round trip), its remainder modulo the list size (the unsigned remainder by the
 // float reciprocal, two corrections) and that member of the list (lane i: is child i listed, how
-// many listed below it); a leaf ends the path (done = 1).  Every level records {node, visits} in
-// path lane Dn.  Stops, without touching the node, where the general step is needed: a table
+// many listed below it); a leaf ends the path (done = 1); the root steps round-robin while its
+// visits do not exceed its children (fc0: its first child).  Every level records {node, visits} in
+// path lane Dn and the node's hidden-state index in par.  Stops, without touching the node, where the general step is needed: a table
 // error or an empty list, a word beyond the stream or the window, the end of the path lanes.
 // rb / tb / cb / wb: the LDS byte addresses of the chase records, the tie-list bits, the tie-list
 // sizes and the engine word of cursor 0 (wo..255: the window's valid slots, cursor + co).
-__device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &nsc, int &xprev, int &px, int &pvv,
+__device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &nsc, int &par, int &px, int &pvv,
                                              int &done, int &leaf_y, int lane, unsigned rb, unsigned tb,
-                                             unsigned cb, unsigned wb, int co, int wo, int cW, int lim) {
-    int t0, t1, t2, t3, t4, t5, t6, va, vb, r0, r1, r2, r3, r4, r5, r6;
+                                             unsigned cb, unsigned wb, int co, int wo, int cW, int lim, int fc0) {
+    int t0, t1, t2, t3, t4, t5, t6, va, vb, r0, r1, r2, r3, r4, r5, r6, r7;
     asm volatile(
         ".Lcl%=_top:\n\t"
         "s_lshl_b32 %[t0], %[x], 4\n\t"
@@ -3892,16 +3910,21 @@ __device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &
         "ds_read_b32 %[r0], %[va]\n\t"
         "ds_read_b32 %[r1], %[va] offset:4\n\t"
         "ds_read_b32 %[r2], %[va] offset:8\n\t"
+        "ds_read_b32 %[r7], %[va] offset:12\n\t"
         "s_add_i32 %[t1], %[dn], 1\n\t"
         "s_waitcnt lgkmcnt(0)\n\t"
         "v_readfirstlane_b32 %[t0], %[r0]\n\t"
         "v_readfirstlane_b32 %[t2], %[r2]\n\t"
         "s_cmp_eq_i32 %[t0], -1\n\t"
         "s_cbranch_scc1 .Lcl%=_leaf\n\t"
-        "s_cmp_ge_i32 %[cur], %[cw]\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
         "s_cmp_ge_i32 %[t1], %[lim]\n\t"
         "s_cbranch_scc1 .Lcl%=_out\n\t"
+        "s_cmp_eq_u32 %[dn], 0\n\t"
+        "s_cbranch_scc1 .Lcl%=_root\n"
+        ".Lcl%=_scored:\n\t"
+        "s_cmp_ge_i32 %[cur], %[cw]\n\t"
+        "s_cbranch_scc1 .Lcl%=_out\n\t"
+        "s_mov_b32 %[t6], 1\n\t"
         "s_cmp_lt_i32 %[t0], 0\n\t"
         "s_cbranch_scc1 .Lcl%=_tie\n"
         ".Lcl%=_step:\n\t"
@@ -3910,13 +3933,23 @@ __device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &
         "s_nop 1\n\t"
         "v_cndmask_b32_e32 %[px], %[px], %[va], vcc\n\t"
         "v_cndmask_b32_e32 %[pv], %[pv], %[r1], vcc\n\t"
+        "v_readfirstlane_b32 %[pa], %[r7]\n\t"
         "s_and_b32 %[t2], %[t2], 0xff\n\t"
         "s_add_i32 %[nsc], %[nsc], %[t2]\n\t"
-        "s_add_i32 %[cur], %[cur], 1\n\t"
-        "s_mov_b32 %[xp], %[x]\n\t"
+        "s_add_i32 %[cur], %[cur], %[t6]\n\t"
         "s_mov_b32 %[x], %[t0]\n\t"
         "s_mov_b32 %[dn], %[t1]\n\t"
         "s_branch .Lcl%=_top\n"
+        ".Lcl%=_root:\n\t"  // forced root round-robin (cnode.cpp:398-399): child visits - 1, no word, not scored
+        "v_readfirstlane_b32 %[t3], %[r1]\n\t"
+        "s_and_b32 %[t4], %[t2], 0xff\n\t"
+        "s_cmp_gt_i32 %[t3], %[t4]\n\t"
+        "s_cbranch_scc1 .Lcl%=_scored\n\t"
+        "s_add_i32 %[t0], %[fc0], %[t3]\n\t"
+        "s_add_i32 %[t0], %[t0], -1\n\t"
+        "s_mov_b32 %[t2], 0\n\t"
+        "s_mov_b32 %[t6], 0\n\t"
+        "s_branch .Lcl%=_step\n"
         ".Lcl%=_tie:\n\t"
         "s_add_i32 %[t3], %[cur], %[co]\n\t"
         "s_cmp_lt_i32 %[t3], %[wo]\n\t"
@@ -3982,6 +4015,7 @@ __device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &
         "s_ff1_i32_b64 %[t5], vcc\n\t"
         "s_sub_i32 %[t0], -2, %[t0]\n\t"
         "s_add_i32 %[t0], %[t0], %[t5]\n\t"
+        "s_mov_b32 %[t6], 1\n\t"
         "s_branch .Lcl%=_step\n"
         ".Lcl%=_leaf:\n\t"
         "v_cmp_eq_u32_e32 vcc, %[dn], %[ln]\n\t"
@@ -3992,13 +4026,13 @@ __device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &
         "s_mov_b32 %[ly], %[t2]\n\t"
         "s_mov_b32 %[dne], 1\n"
         ".Lcl%=_out:"
-        : [x] "+s"(x), [dn] "+s"(Dn), [cur] "+s"(cursor), [nsc] "+s"(nsc), [xp] "+s"(xprev), [px] "+v"(px),
+        : [x] "+s"(x), [dn] "+s"(Dn), [cur] "+s"(cursor), [nsc] "+s"(nsc), [pa] "+s"(par), [px] "+v"(px),
           [pv] "+v"(pvv), [dne] "+s"(done), [ly] "+s"(leaf_y), [t0] "=&s"(t0), [t1] "=&s"(t1), [t2] "=&s"(t2),
           [t3] "=&s"(t3), [t4] "=&s"(t4), [t5] "=&s"(t5), [t6] "=&s"(t6), [va] "=&v"(va), [vb] "=&v"(vb),
           [r0] "=&v"(r0), [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4), [r5] "=&v"(r5),
-          [r6] "=&v"(r6)
+          [r6] "=&v"(r6), [r7] "=&v"(r7)
         : [rb] "s"(rb), [tb] "s"(tb), [cb] "s"(cb), [wb] "s"(wb), [co] "s"(co), [wo] "s"(wo), [cw] "s"(cW),
-          [lim] "s"(lim), [ln] "v"(lane)
+          [lim] "s"(lim), [ln] "v"(lane), [fc0] "s"(fc0)
         : "vcc", "scc", "memory");
 }
 
@@ -4006,15 +4040,15 @@ template <int NC>
 __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
                                                  int D, unsigned long long *tp = nullptr) {
     using L = TreeLayout<NC>;
-    static_assert(NC <= 512, "two nodes per lane and pass, 128-entry lists");
+    static_assert(NC <= 512, "at most two nodes per lane and pass, 128-entry lists");
+    (void)disc;
     const int l = lane_id();
     const int4 *sA = (const int4 *)(smem + L::oA);
     const int4 *sB = (const int4 *)(smem + L::oB);
-    const float *sPP = (const float *)(smem + L::oPP);
     float *sSc = (float *)(smem + L::oPS);
     const int *sFl = (const int *)(smem + L::oFl);
-    float2 *sAz = (float2 *)(smem + L::oAz);  // (S1) inputs; (S2) tie-list bits
-    int *sQ = (int *)(smem + L::oQ);          // (S2) tie-list size | table error << 16
+    float2 *sAz = (float2 *)(smem + L::oAz);  // (S2) tie-list bits
+    int *sQ = (int *)(smem + L::oQ);          // (S1) every visited node's q; (S2) tie-list size | table error << 16
     int4 *sRec = (int4 *)(smem + L::oCn);     // chase records (the value-set scalars are consumed)
     int4 *sLst = (int4 *)(smem + L::oReg) + wv * 2 * kWave;  // (the value entries are consumed)
     const float *xf = (const float *)(smem + L::oX);
@@ -4028,37 +4062,37 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
         const float delta = mmx - mmn;
         den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
     }
-    // (S1), both of the lane's nodes at once
-    int nn[2], nfl[2];
-    int4 na[2], nb[2];
-    float npp[2];
-    float2 naz[2];
+    // (S1), both of the lane's nodes at once, every load up front (addresses clamped to the class,
+    // not to ntot, so they do not wait for the exchanged error words).  A visited node's q --
+    // get_qsa - father->pred_value, (reward + discount * value) - pred_value -- is its stored one
+    // off the path (the value has not changed since) and the back-propagation's new one on it
+    // (staged into sQ by bk_levels)
+    constexpr int NU = (NC + 4 * kWave - 1) / (4 * kWave);  // nodes per lane: 1 up to 256 nodes, else 2
+    int nn[NU], nfl[NU], nvx[NU];
+    int4 nb[NU];
+    float nq[NU], npr[NU];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NU; ++u) {
         nn[u] = wv * kWave + l + 4 * kWave * u;
-        const int n = nn[u] < ntot ? nn[u] : 0;
-        na[u] = sA[n];
+        const int n = nn[u] < NC ? nn[u] : 0;
+        nvx[u] = sA[n].x;
         nb[u] = sB[n];
         nfl[u] = sFl[n];
-        naz[u] = sAz[n];
-        npp[u] = sPP[n];
+        nq[u] = i2f(sQ[n]);
+        npr[u] = sSc[n];
     }
     int cnt_list = 0;
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < NU; ++u) {
         const int n = nn[u];
         const bool in = n < ntot;
-        const int fl = nfl[u];
-        const int vis = na[u].x + (fl ? 1 : 0);
-        if (in && n >= 1) {
-            const float val = fl ? naz[u].x : i2f(na[u].z);
-            const float rw = fl ? naz[u].y : i2f(na[u].w);
-            float vs = (vis == 0) ? 0.0f : ((rw + disc * val) - npp[u]);
-            if (mm_on) vs = (vs - mmn) / den;
-            if (vs < 0) vs = 0;
-            if (vs > 1) vs = 1;
-            sSc[n] = sSc[n] + vs;  // prior_score + value_score
-        }
+        const int vis = nvx[u] + (nfl[u] ? 1 : 0);
+        float vs = (vis == 0) ? 0.0f : nq[u];
+        if (mm_on) vs = (vs - mmn) / den;
+        if (vs < 0) vs = 0;
+        if (vs > 1) vs = 1;
+        const float sc = npr[u] + vs;  // prior_score + value_score
+        if (in && n >= 1) sSc[n] = sc;
         const int nc = nc_of(nb[u].y);
         if (in) sRec[n] = make_int4(nc == 0 ? kTreeLeaf : 0, vis, nb[u].y, nb[u].w);
         const bool par = in && nc > 0;
@@ -4078,24 +4112,48 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
             const int p = pe.x, fc = pe.y, nc = pe.z;
             const int np = pe.w - 1;  // total_children_visit_counts
             const bool terr = np < 0 || np >= PS;
-            float mx = -1000000.0f;  // FLOAT_MIN (utils.h:12)
             unsigned long long lst = 0ull;
             int cnt = 0;
-            for (int i0 = 0; i0 < nc; i0 += 8) {
+            if (nc <= 8) {
+                // the sequential arg-max in closed form (as the level walk): the first maximum and
+                // every later child within epsilon of it; {s >= FLOAT_MIN} when no score beats FLOAT_MIN
                 float sc[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + ((i0 + u < nc) ? i0 + u : i0)];
+                for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + (u < nc ? u : 0)];
+                float M = -INFINITY;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) M = (u < nc) ? fmaxf(M, sc[u]) : M;
+                unsigned m = 0u, eq = 0u, fm = 0u;
+                const float thr = M - 0.000001f;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    const int i = i0 + u;
-                    const float v = sc[u];
-                    const bool ok = i < nc;
-                    const bool gt = ok && (mx < v);
-                    const bool ge = ok && !gt && (v >= mx - 0.000001f);
-                    const unsigned long long bit = 1ull << (i & 63);
-                    lst = gt ? bit : (ge ? (lst | bit) : lst);
-                    cnt = gt ? 1 : (cnt + (ge ? 1 : 0));
-                    mx = gt ? v : mx;
+                    const bool ok = u < nc;
+                    eq |= (ok && sc[u] == M) ? 1u << u : 0u;
+                    m |= (ok && sc[u] >= thr) ? 1u << u : 0u;
+                    fm |= (ok && sc[u] >= -1000000.0f) ? 1u << u : 0u;
+                }
+                const unsigned below_first = (eq & (0u - eq)) - 1u;  // the bits below the first maximum
+                const unsigned b32 = (M > -1000000.0f) ? (m & ~below_first) : fm;
+                lst = b32;
+                cnt = __popc(b32);
+            } else {
+                float mx = -1000000.0f;  // FLOAT_MIN (utils.h:12)
+                for (int i0 = 0; i0 < nc; i0 += 8) {
+                    float sc[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + ((i0 + u < nc) ? i0 + u : i0)];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int i = i0 + u;
+                        const float v = sc[u];
+                        const bool ok = i < nc;
+                        const bool gt = ok && (mx < v);
+                        const bool ge = ok && !gt && (v >= mx - 0.000001f);
+                        const unsigned long long bit = 1ull << (i & 63);
+                        lst = gt ? bit : (ge ? (lst | bit) : lst);
+                        cnt = gt ? 1 : (cnt + (ge ? 1 : 0));
+                        mx = gt ? v : mx;
+                    }
                 }
             }
             const bool one = cnt == 1 && !terr;
@@ -4221,6 +4279,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         s.A = sA;
         s.B = sB;
         s.PP = sPP;
+        s.Q = sQ;
         s.path = sPath;
         s.lp = sLp;
         float *boot = (float *)(smem + L::oBoot) + (wv - 1) * (L::PSx + kWave);
@@ -4341,6 +4400,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         s.A = sA;
         s.B = sB;
         s.PP = sPP;
+        s.Q = sQ;
         s.path = sPath;
         s.lp = sLp;
         float *boot = (float *)(smem + L::oBoot);
@@ -4570,15 +4630,48 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
     const long long ent_r = xl[0] + xl[11] + xl[13], ent_w = xl[1] + xl[12] + xl[14];
     const int ntot = err ? tot : tot + ncl;
+    const int fc0 = uni(sB[0].x);  // the root's first child (its round-robin), read with (S1)'s records
     unsigned long long tp[4] = {0};
     unsigned long long trep = 0;
     (void)trep;
+    unsigned long long cal[3] = {0, 0, 0};
+    (void)cal;
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
     long long nscored = 0;
     int px = 0, pvv = 0;  // level i's node (and, by levels, its visits) in lane i; sPath past 64 levels
     if constexpr (!SEL) {
         stamp(ts, 5);
     } else {
+#ifdef MZ_DIAG_CAL  // calibration: 16 dependent LDS reads, 64 dependent VALU ops, 64 dependent SALU ops
+        {
+            int v = l & 1;
+            const int *sI = (const int *)(smem + L::oX);
+            unsigned long long c0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            c0 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                v = sI[v & 3];
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) :: "memory");
+                v &= 1;
+            }
+            unsigned long long c1 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int k = 0; k < 64; ++k) asm volatile("v_add_u32 %0, %0, 1" : "+v"(v));
+            unsigned long long c2 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            int sv = uni(v);
+#pragma unroll
+            for (int k = 0; k < 64; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sv));
+            unsigned long long c3 = __builtin_amdgcn_s_memtime();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            cal[0] = c1 - c0;
+            cal[1] = c2 - c1;
+            cal[2] = c3 - c2 + (unsigned long long)((sv + v) & 0);
+        }
+#endif
         // below the 1024-node class the four waves prepare every expanded node's outcome first
         if constexpr (!kTreeLevels<NC>) tree_select_prep<NC>(smem, 0, ntot, discount, gdelta, PS, D, tp);
         stamp(ts, 5);
@@ -4594,8 +4687,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         // parameter block every level (constant loads rematerialise under SGPR pressure)
         int cW = gW, cPS = PS, cwo = wsh - wbase;
         asm volatile("" : "+s"(cW), "+s"(cPS), "+s"(cwo));
-        const int fc0 = uni(sB[0].x);
-        int xprev = 0, nsc = 0, done = 0;
+        int par_hsx = 0, nsc = 0, done = 0;
         const int lim = cPS < kWave ? cPS : kWave;
         const unsigned rb = lds_addr(smem) + L::oCn, tb = lds_addr(smem) + L::oAz, cb = lds_addr(smem) + L::oQ,
                        wb = lds_addr(smem) + L::oRng;
@@ -4615,10 +4707,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         }
 #endif
         while (true) {
-            if (Dn > 0) {
-                chase_levels(x, Dn, cursor, nsc, xprev, px, pvv, done, leaf_y, l, rb, tb, cb, wb, cwo, wsh, cW, lim);
-                if (done) break;
-            }
+            chase_levels(x, Dn, cursor, nsc, par_hsx, px, pvv, done, leaf_y, l, rb, tb, cb, wb, cwo, wsh, cW, lim, fc0);
+            if (done) break;
             // the general step
             x = uni(x);
             cursor = uni(cursor);
@@ -4664,7 +4754,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             }
             nscored += forced ? 0 : nc;
             cursor += consume;
-            xprev = x;
+            par_hsx = uni(rec.w);
             x = next;
             ++Dn;
         }
@@ -4673,7 +4763,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
 #endif
         nscored += nsc;
         if (Dn == 0) err |= kErrRoot;
-        out_idx = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
+        out_idx = Dn == 0 ? uni(sB[0].w) : par_hsx;  // parent->hidden_state_index_x
         out_act = act_of(leaf_y);                      // children_action of the last edge
     }
     if (!err && kTreeLevels<NC>) {
@@ -4893,6 +4983,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             case MZ_S_CYC_BAK_WAIT: add = tp[0] ? (long long)(tp[0] - ts[4]) : 0; break;  // (S1)
             default: break;
         }
+#ifdef MZ_DIAG_CAL
+        if (l == MZ_S_CYC_STAGE1) add = (long long)cal[0];
+        if (l == MZ_S_CYC_STAGE2) add = (long long)cal[1];
+        if (l == MZ_S_CYC_W1_STAGE2) add = (long long)cal[2];
+#endif
 #ifdef MZ_DIAG_TWICE  // the chase's first and second pass
         if (l == MZ_S_CYC_STAGE1) add = trep ? (long long)(trep - ts[5]) : 0;
         if (l == MZ_S_CYC_STAGE2) add = trep ? (long long)(ts[6] - trep) : 0;
