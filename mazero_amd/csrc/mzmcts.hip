@@ -3766,38 +3766,23 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         const int by = uni(b4.y);
         // entries of a smaller depth / the same depth / the same depth and a smaller value; none but
         // smaller depths when the node's deepest entry is above dep (stage_regions' need test)
-        // (up to 64 entries, the usual case: one register per lane, read once; the two order
-        // statistics by readlane and the tail shift from registers)
-        const bool one = nv <= kWave;
-        int2 e1 = make_int2(0x7fffffff, 0);
-        if (one && l < nv) e1 = R[l];
         int lo = nv, c = 0, pv = 0;
         if (nv > 0 && md_of(by) >= dep) {
             lo = 0;
-            if (one) {
-                const bool on = l < nv;
-                lo = __popcll(ballot(on && e1.x < dep));
-                c = __popcll(ballot(on && e1.x == dep));
-                pv = __popcll(ballot(on && e1.x == dep && i2f(e1.y) < key));
-            } else {
-                for (int e0 = 0; e0 < nv; e0 += kWave) {
-                    const bool on = e0 + l < nv;
-                    const int2 e = on ? R[e0 + l] : make_int2(0x7fffffff, 0);
-                    lo += __popcll(ballot(on && e.x < dep));
-                    c += __popcll(ballot(on && e.x == dep));
-                    pv += __popcll(ballot(on && e.x == dep && i2f(e.y) < key));
-                }
+            for (int e0 = 0; e0 < nv; e0 += kWave) {
+                const bool on = e0 + l < nv;
+                const int2 e = on ? R[e0 + l] : make_int2(0x7fffffff, 0);
+                lo += __popcll(ballot(on && e.x < dep));
+                c += __popcll(ballot(on && e.x == dep));
+                pv += __popcll(ballot(on && e.x == dep && i2f(e.y) < key));
             }
             ent_r += nv;
         }
-#ifdef MZ_DIAG_BK
-        if (tl && j == 0) tl[4] = __builtin_amdgcn_s_memtime();
-#endif
         float ws = cw.x, tw = cw.y;
         const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
         const int nl = value_lim(c + 1, g.one_minus_rho);
         if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
-            const float mb = one ? rlf(i2f(e1.y), lo + c - cur) : i2f(R[lo + c - cur].y);  // *big.begin()
+            const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
             if (!(key < mb)) {
                 ws -= lp * mb;
                 tw -= lp;
@@ -3810,7 +3795,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
                 tw += lp;
                 ws += lp * key;
             } else {
-                const float ms = one ? rlf(i2f(e1.y), lo + c - cur - 1) : i2f(R[lo + c - cur - 1].y);  // *(--small.end())
+                const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
                 if (key > ms) {
                     tw += lp;
                     ws += lp * key;
@@ -3820,9 +3805,6 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
                 }
             }
         }
-#ifdef MZ_DIAG_BK
-        if (tl && j == 0) tl[5] = __builtin_amdgcn_s_memtime();
-#endif
         int pos = lo + pv;
         int2 *G = gV + (size_t)n * g.E;
         if (nv + 1 > g.E) {
@@ -3831,12 +3813,8 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         } else if (l == 0) {
             G[pos] = make_int2(dep, f2i(key));
         }
-        if (one) {  // the entries after the insertion point move up by one
-            if (l >= pos && l < nv) G[l + 1] = e1;
-        } else {
-            for (int e0 = pos; e0 < nv; e0 += kWave)
-                if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
-        }
+        for (int e0 = pos; e0 < nv; e0 += kWave)  // the entries after the insertion point move up by one
+            if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
         ent_w += nv - pos + 1;
         const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
         int4 a4 = a4r;
@@ -3846,16 +3824,12 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         const size_t gi = (size_t)t * g.P + n;
         float q = 0.f;
         if (i >= 1) q = (i2f(a4.w) + disc * val) - ppn;  // get_qsa - father->pred_value
-#ifdef MZ_DIAG_BK
-        if (tl && j == 0) tl[6] = __builtin_amdgcn_s_memtime() + (unsigned long long)(f2i(q) & 0);
-#endif
         if (l == 0) {
             d.A()[gi] = make_int4(a4.x + 1, a4.y, f2i(val), a4.w);
             d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
             if (!is_leaf && dep > md_of(by)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(by), dep), b4.z, b4.w);
             if (i >= 1) d.Q()[gi] = q;
             sAz[n] = make_float2(val, i2f(a4.w));
-            if (i >= 1 && s.Q) s.Q[n] = q;  // the staged copy too (k_tree's scores; its min/max skips path nodes)
         }
         if (i >= 1) {
             pmn = fminf(pmn, q);
@@ -3865,192 +3839,38 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
     }
 }
 
-// k_tree after barrier (2), run by all four waves; wave w owns nodes w * 64 + l + 256 j:
+// k_tree after barrier (2), run by all four waves (64-node blocks dealt round-robin):
 //  (S1) every node's ucb score under its parent (cnode.cpp:297-335) -- the prior score of waves 2
 //       and 3 plus the value score, min/max-normalised with the joined min/max -- in place of the
-//       prior score, two nodes per lane in one pass; every node's chase record {outcome, visits,
-//       structure word, hidden-state index}; the wave's expanded nodes (nc > 0, at most sims + 1 in
-//       the whole tree) compacted into a list with what (S2) needs of them;
-//  (S2) after barrier (3), the select_child outcome (cnode.cpp:337-379) of every listed node: the
-//       reference's sequential arg-max with epsilon ties over its children's scores.  The outcome is
-//       the child when the list has one member and the parent is inside the pUCT table, otherwise
-//       kSlowBase - first child, with the list bits and size | table error << 16 aside (ties, an
-//       empty list, a table error: wave 0 resolves those with the engine word at its cursor).
-// After barrier (4) wave 0 chases the outcomes from the root: one LDS round trip per level (the
-// node's chase record and the level's engine word).
-constexpr int kTreeLeaf = -1, kSlowBase = -2;
+//       prior score;
+//  (S2) every node's select_child outcome (cnode.cpp:337-379): the reference's sequential arg-max
+//       with epsilon ties over its children's scores.  A one-child tie list (the usual case) is
+//       stored as the next node (sPar, free now); leaves get kTreeLeaf; other lists (ties, an empty
+//       list, a parent beyond the pUCT table) get kTreeSlow and an exact record: list bits in sAz,
+//       size | table error << 16 in sQ.
+// Wave 0 then chases next nodes one LDS read per level.
+constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 
-// The 1024-node class walks level by level instead, scoring on the walk (O(depth) after barrier
-// (2) instead of O(pool) / 4 waves).  Measured on one box, k_tree fused launch, before the two-node
-// pass and the node lists: 27m K = 5 (1010 nodes) 13.8 us by levels against 14.1 us; 3m K = 5 (260
-// nodes) 10.4 against 11.6 us, 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
+// The 1024-node class walks level by level instead (O(depth) after the barrier instead of
+// O(pool) / 4 waves).  Measured on one box, k_tree fused launch: 27m K = 5 (1010 nodes) 13.8 us by
+// levels against 14.1 us with tree_select_prep; 3m K = 5 (260 nodes) 10.4 against 11.6 us,
+// 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
 template <int NC>
 constexpr bool kTreeLevels = (NC >= 1024);
-
-// The chase's levels (wave 0, uniform control flow), one LDS round trip and ~25 instructions a
-// level: a node whose outcome is a child (a one-member list inside the table) steps to it; a tie
-// (an exact record with two or more members) takes the engine word at the cursor from the LDS
-// window (one more round trip), its remainder modulo the list size (the unsigned remainder by the
-// float reciprocal, two corrections) and that member of the list (lane i: is child i listed, how
-// many listed below it); a leaf ends the path (done = 1); the root steps round-robin while its
-// visits do not exceed its children (fc0: its first child).  Every level records {node, visits} in
-// path lane Dn and the node's hidden-state index in par.  Stops, without touching the node, where the general step is needed: a table
-// error or an empty list, a word beyond the stream or the window, the end of the path lanes.
-// rb / tb / cb / wb: the LDS byte addresses of the chase records, the tie-list bits, the tie-list
-// sizes and the engine word of cursor 0 (wo..255: the window's valid slots, cursor + co).
-__device__ __forceinline__ void chase_levels(int &x, int &Dn, int &cursor, int &nsc, int &par, int &px, int &pvv,
-                                             int &done, int &leaf_y, int lane, unsigned rb, unsigned tb,
-                                             unsigned cb, unsigned wb, int co, int wo, int cW, int lim, int fc0) {
-    int t0, t1, t2, t3, t4, t5, t6, va, vb, r0, r1, r2, r3, r4, r5, r6, r7;
-    asm volatile(
-        ".Lcl%=_top:\n\t"
-        "s_lshl_b32 %[t0], %[x], 4\n\t"
-        "s_add_u32 %[t0], %[t0], %[rb]\n\t"
-        "v_mov_b32 %[va], %[t0]\n\t"
-        "ds_read_b32 %[r0], %[va]\n\t"
-        "ds_read_b32 %[r1], %[va] offset:4\n\t"
-        "ds_read_b32 %[r2], %[va] offset:8\n\t"
-        "ds_read_b32 %[r7], %[va] offset:12\n\t"
-        "s_add_i32 %[t1], %[dn], 1\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_readfirstlane_b32 %[t0], %[r0]\n\t"
-        "v_readfirstlane_b32 %[t2], %[r2]\n\t"
-        "s_cmp_eq_i32 %[t0], -1\n\t"
-        "s_cbranch_scc1 .Lcl%=_leaf\n\t"
-        "s_cmp_ge_i32 %[t1], %[lim]\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
-        "s_cmp_eq_u32 %[dn], 0\n\t"
-        "s_cbranch_scc1 .Lcl%=_root\n"
-        ".Lcl%=_scored:\n\t"
-        "s_cmp_ge_i32 %[cur], %[cw]\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
-        "s_mov_b32 %[t6], 1\n\t"
-        "s_cmp_lt_i32 %[t0], 0\n\t"
-        "s_cbranch_scc1 .Lcl%=_tie\n"
-        ".Lcl%=_step:\n\t"
-        "v_cmp_eq_u32_e32 vcc, %[dn], %[ln]\n\t"
-        "v_mov_b32 %[va], %[x]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e32 %[px], %[px], %[va], vcc\n\t"
-        "v_cndmask_b32_e32 %[pv], %[pv], %[r1], vcc\n\t"
-        "v_readfirstlane_b32 %[pa], %[r7]\n\t"
-        "s_and_b32 %[t2], %[t2], 0xff\n\t"
-        "s_add_i32 %[nsc], %[nsc], %[t2]\n\t"
-        "s_add_i32 %[cur], %[cur], %[t6]\n\t"
-        "s_mov_b32 %[x], %[t0]\n\t"
-        "s_mov_b32 %[dn], %[t1]\n\t"
-        "s_branch .Lcl%=_top\n"
-        ".Lcl%=_root:\n\t"  // forced root round-robin (cnode.cpp:398-399): child visits - 1, no word, not scored
-        "v_readfirstlane_b32 %[t3], %[r1]\n\t"
-        "s_and_b32 %[t4], %[t2], 0xff\n\t"
-        "s_cmp_gt_i32 %[t3], %[t4]\n\t"
-        "s_cbranch_scc1 .Lcl%=_scored\n\t"
-        "s_add_i32 %[t0], %[fc0], %[t3]\n\t"
-        "s_add_i32 %[t0], %[t0], -1\n\t"
-        "s_mov_b32 %[t2], 0\n\t"
-        "s_mov_b32 %[t6], 0\n\t"
-        "s_branch .Lcl%=_step\n"
-        ".Lcl%=_tie:\n\t"
-        "s_add_i32 %[t3], %[cur], %[co]\n\t"
-        "s_cmp_lt_i32 %[t3], %[wo]\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
-        "s_cmpk_gt_i32 %[t3], 0xff\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
-        "s_lshl_b32 %[t3], %[t3], 2\n\t"
-        "s_add_u32 %[t3], %[t3], %[wb]\n\t"
-        "v_mov_b32 %[vb], %[t3]\n\t"
-        "ds_read_b32 %[r3], %[vb]\n\t"
-        "s_lshl_b32 %[t3], %[x], 2\n\t"
-        "s_add_u32 %[t3], %[t3], %[cb]\n\t"
-        "v_mov_b32 %[vb], %[t3]\n\t"
-        "ds_read_b32 %[r4], %[vb]\n\t"
-        "s_lshl_b32 %[t3], %[x], 3\n\t"
-        "s_add_u32 %[t3], %[t3], %[tb]\n\t"
-        "v_mov_b32 %[vb], %[t3]\n\t"
-        "ds_read_b32 %[r5], %[vb]\n\t"
-        "ds_read_b32 %[r6], %[vb] offset:4\n\t"
-        "s_waitcnt lgkmcnt(0)\n\t"
-        "v_readfirstlane_b32 %[t3], %[r4]\n\t"
-        "s_cmpk_gt_u32 %[t3], 0xffff\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
-        "s_cmp_lt_u32 %[t3], 2\n\t"
-        "s_cbranch_scc1 .Lcl%=_out\n\t"
-        // t4 = w % t3
-        "v_readfirstlane_b32 %[t4], %[r3]\n\t"
-        "v_cvt_f32_u32_e32 %[vb], %[t3]\n\t"
-        "v_rcp_iflag_f32_e32 %[vb], %[vb]\n\t"
-        "s_nop 1\n\t"
-        "v_mul_f32_e32 %[vb], 0x4f7ffffe, %[vb]\n\t"
-        "v_cvt_u32_f32_e32 %[vb], %[vb]\n\t"
-        "s_nop 1\n\t"
-        "v_readfirstlane_b32 %[t5], %[vb]\n\t"
-        "s_sub_i32 %[t6], 0, %[t3]\n\t"
-        "s_mul_i32 %[t6], %[t6], %[t5]\n\t"
-        "s_mul_hi_u32 %[t6], %[t5], %[t6]\n\t"
-        "s_add_i32 %[t5], %[t5], %[t6]\n\t"
-        "s_mul_hi_u32 %[t6], %[t4], %[t5]\n\t"
-        "s_mul_i32 %[t6], %[t6], %[t3]\n\t"
-        "s_sub_i32 %[t4], %[t4], %[t6]\n\t"
-        "s_sub_i32 %[t6], %[t4], %[t3]\n\t"
-        "s_cmp_ge_u32 %[t4], %[t3]\n\t"
-        "s_cselect_b32 %[t4], %[t6], %[t4]\n\t"
-        "s_sub_i32 %[t6], %[t4], %[t3]\n\t"
-        "s_cmp_ge_u32 %[t4], %[t3]\n\t"
-        "s_cselect_b32 %[t4], %[t6], %[t4]\n\t"
-        // the t4-th listed child: lane i listed (bit i of {r6:r5}) with t4 listed below it
-        "v_readfirstlane_b32 %[t5], %[r5]\n\t"
-        "v_readfirstlane_b32 %[t6], %[r6]\n\t"
-        "v_cmp_gt_u32_e32 vcc, 32, %[ln]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e32 %[vb], %[r6], %[r5], vcc\n\t"
-        "v_lshrrev_b32_e32 %[vb], %[ln], %[vb]\n\t"
-        "v_and_b32_e32 %[vb], 1, %[vb]\n\t"
-        "v_xor_b32_e32 %[vb], 1, %[vb]\n\t"
-        "v_lshlrev_b32_e32 %[vb], 31, %[vb]\n\t"
-        "v_mbcnt_lo_u32_b32 %[va], %[t5], 0\n\t"
-        "v_mbcnt_hi_u32_b32 %[va], %[t6], %[va]\n\t"
-        "v_or_b32_e32 %[va], %[va], %[vb]\n\t"
-        "v_cmp_eq_u32_e32 vcc, %[t4], %[va]\n\t"
-        "s_nop 4\n\t"
-        "s_ff1_i32_b64 %[t5], vcc\n\t"
-        "s_sub_i32 %[t0], -2, %[t0]\n\t"
-        "s_add_i32 %[t0], %[t0], %[t5]\n\t"
-        "s_mov_b32 %[t6], 1\n\t"
-        "s_branch .Lcl%=_step\n"
-        ".Lcl%=_leaf:\n\t"
-        "v_cmp_eq_u32_e32 vcc, %[dn], %[ln]\n\t"
-        "v_mov_b32 %[va], %[x]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e32 %[px], %[px], %[va], vcc\n\t"
-        "v_cndmask_b32_e32 %[pv], %[pv], %[r1], vcc\n\t"
-        "s_mov_b32 %[ly], %[t2]\n\t"
-        "s_mov_b32 %[dne], 1\n"
-        ".Lcl%=_out:"
-        : [x] "+s"(x), [dn] "+s"(Dn), [cur] "+s"(cursor), [nsc] "+s"(nsc), [pa] "+s"(par), [px] "+v"(px),
-          [pv] "+v"(pvv), [dne] "+s"(done), [ly] "+s"(leaf_y), [t0] "=&s"(t0), [t1] "=&s"(t1), [t2] "=&s"(t2),
-          [t3] "=&s"(t3), [t4] "=&s"(t4), [t5] "=&s"(t5), [t6] "=&s"(t6), [va] "=&v"(va), [vb] "=&v"(vb),
-          [r0] "=&v"(r0), [r1] "=&v"(r1), [r2] "=&v"(r2), [r3] "=&v"(r3), [r4] "=&v"(r4), [r5] "=&v"(r5),
-          [r6] "=&v"(r6), [r7] "=&v"(r7)
-        : [rb] "s"(rb), [tb] "s"(tb), [cb] "s"(cb), [wb] "s"(wb), [co] "s"(co), [wo] "s"(wo), [cw] "s"(cW),
-          [lim] "s"(lim), [ln] "v"(lane), [fc0] "s"(fc0)
-        : "vcc", "scc", "memory");
-}
 
 template <int NC>
 __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
                                                  int D, unsigned long long *tp = nullptr) {
     using L = TreeLayout<NC>;
-    static_assert(NC <= 512, "at most two nodes per lane and pass, 128-entry lists");
-    (void)disc;
     const int l = lane_id();
     const int4 *sA = (const int4 *)(smem + L::oA);
     const int4 *sB = (const int4 *)(smem + L::oB);
+    const float *sPP = (const float *)(smem + L::oPP);
+    float *sQ = (float *)(smem + L::oQ);
+    int *nxt = (int *)(smem + L::oPar);
     float *sSc = (float *)(smem + L::oPS);
     const int *sFl = (const int *)(smem + L::oFl);
-    float2 *sAz = (float2 *)(smem + L::oAz);  // (S2) tie-list bits
-    int *sQ = (int *)(smem + L::oQ);          // (S1) every visited node's q; (S2) tie-list size | table error << 16
-    int4 *sRec = (int4 *)(smem + L::oCn);     // chase records (the value-set scalars are consumed)
-    int4 *sLst = (int4 *)(smem + L::oReg) + wv * 2 * kWave;  // (the value entries are consumed)
+    float2 *sAz = (float2 *)(smem + L::oAz);
     const float *xf = (const float *)(smem + L::oX);
     const int *xi = (const int *)(smem + L::oX);
     const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), unif(xf[4]));
@@ -4062,88 +3882,46 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
         const float delta = mmx - mmn;
         den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
     }
-    // (S1), both of the lane's nodes at once, every load up front (addresses clamped to the class,
-    // not to ntot, so they do not wait for the exchanged error words).  A visited node's q --
-    // get_qsa - father->pred_value, (reward + discount * value) - pred_value -- is its stored one
-    // off the path (the value has not changed since) and the back-propagation's new one on it
-    // (staged into sQ by bk_levels)
-    constexpr int NU = (NC + 4 * kWave - 1) / (4 * kWave);  // nodes per lane: 1 up to 256 nodes, else 2
-    int nn[NU], nfl[NU], nvx[NU];
-    int4 nb[NU];
-    float nq[NU], npr[NU];
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        nn[u] = wv * kWave + l + 4 * kWave * u;
-        const int n = nn[u] < NC ? nn[u] : 0;
-        nvx[u] = sA[n].x;
-        nb[u] = sB[n];
-        nfl[u] = sFl[n];
-        nq[u] = i2f(sQ[n]);
-        npr[u] = sSc[n];
-    }
-    int cnt_list = 0;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        const int n = nn[u];
-        const bool in = n < ntot;
-        const int vis = nvx[u] + (nfl[u] ? 1 : 0);
-        float vs = (vis == 0) ? 0.0f : nq[u];
-        if (mm_on) vs = (vs - mmn) / den;
-        if (vs < 0) vs = 0;
-        if (vs > 1) vs = 1;
-        const float sc = npr[u] + vs;  // prior_score + value_score
-        if (in && n >= 1) sSc[n] = sc;
-        const int nc = nc_of(nb[u].y);
-        if (in) sRec[n] = make_int4(nc == 0 ? kTreeLeaf : 0, vis, nb[u].y, nb[u].w);
-        const bool par = in && nc > 0;
-        const unsigned long long m = ballot(par);
-        const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        if (par) sLst[cnt_list + below] = make_int4(n, nb[u].x, nc, vis);
-        cnt_list += (int)__popcll(m);
+    for (int n0 = wv * kWave; n0 < ntot; n0 += 4 * kWave) {  // (S1)
+        const int n = n0 + l;
+        if (n >= 1 && n < ntot) {
+            const int4 a = sA[n];
+            const int fl = sFl[n];
+            const float2 az = sAz[n];
+            const int vis = a.x + (fl ? 1 : 0);
+            const float val = fl ? az.x : i2f(a.z);
+            const float rw = fl ? az.y : i2f(a.w);
+            float vs = (vis == 0) ? 0.0f : ((rw + disc * val) - sPP[n]);
+            if (mm_on) vs = (vs - mmn) / den;
+            if (vs < 0) vs = 0;
+            if (vs > 1) vs = 1;
+            sSc[n] = sSc[n] + vs;  // prior_score + value_score
+        }
     }
     if (MZ_STAMPS && tp) {
         wait_lds();
         tp[0] = __builtin_amdgcn_s_memtime();
     }
     lds_barrier();  // (3)
-    for (int e0 = 0; e0 < cnt_list; e0 += kWave) {  // (S2)
-        if (e0 + l < cnt_list) {
-            const int4 pe = sLst[e0 + l];
-            const int p = pe.x, fc = pe.y, nc = pe.z;
-            const int np = pe.w - 1;  // total_children_visit_counts
-            const bool terr = np < 0 || np >= PS;
-            unsigned long long lst = 0ull;
-            int cnt = 0;
-            if (nc <= 8) {
-                // the sequential arg-max in closed form (as the level walk): the first maximum and
-                // every later child within epsilon of it; {s >= FLOAT_MIN} when no score beats FLOAT_MIN
-                float sc[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + (u < nc ? u : 0)];
-                float M = -INFINITY;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) M = (u < nc) ? fmaxf(M, sc[u]) : M;
-                unsigned m = 0u, eq = 0u, fm = 0u;
-                const float thr = M - 0.000001f;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const bool ok = u < nc;
-                    eq |= (ok && sc[u] == M) ? 1u << u : 0u;
-                    m |= (ok && sc[u] >= thr) ? 1u << u : 0u;
-                    fm |= (ok && sc[u] >= -1000000.0f) ? 1u << u : 0u;
-                }
-                const unsigned below_first = (eq & (0u - eq)) - 1u;  // the bits below the first maximum
-                const unsigned b32 = (M > -1000000.0f) ? (m & ~below_first) : fm;
-                lst = b32;
-                cnt = __popc(b32);
+    for (int p0 = wv * kWave; p0 < ntot; p0 += 4 * kWave) {  // (S2)
+        const int p = p0 + l;
+        if (p < ntot) {
+            const int4 b = sB[p];
+            const int fc = b.x, nc = nc_of(b.y);
+            if (nc == 0) {
+                nxt[p] = kTreeLeaf;
             } else {
+                const int np = sA[p].x + (sFl[p] ? 1 : 0) - 1;  // total_children_visit_counts
+                const bool terr = np < 0 || np >= PS;
                 float mx = -1000000.0f;  // FLOAT_MIN (utils.h:12)
-                for (int i0 = 0; i0 < nc; i0 += 8) {
-                    float sc[8];
+                unsigned long long lst = 0ull;
+                int cnt = 0;
+                for (int i0 = 0; i0 < nc; i0 += 4) {
+                    float sc[4];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + ((i0 + u < nc) ? i0 + u : i0)];
+                    for (int u = 0; u < 4; ++u) sc[u] = sSc[fc + ((i0 + u < nc) ? i0 + u : i0)];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) {
+                    for (int u = 0; u < 4; ++u) {
                         const int i = i0 + u;
                         const float v = sc[u];
                         const bool ok = i < nc;
@@ -4155,12 +3933,13 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
                         mx = gt ? v : mx;
                     }
                 }
-            }
-            const bool one = cnt == 1 && !terr;
-            ((int *)sRec)[4 * p] = one ? fc + (int)__builtin_ctzll(lst) : kSlowBase - fc;
-            if (!one) {
-                sAz[p] = make_float2(i2f((int)(unsigned)(lst & 0xffffffffull)), i2f((int)(unsigned)(lst >> 32)));
-                sQ[p] = cnt | (terr ? 0x10000 : 0);
+                if (cnt == 1 && !terr) {
+                    nxt[p] = fc + __builtin_ctzll(lst);
+                } else {
+                    nxt[p] = kTreeSlow;
+                    sAz[p] = make_float2(i2f((int)(unsigned)(lst & 0xffffffffull)), i2f((int)(unsigned)(lst >> 32)));
+                    sQ[p] = i2f(cnt | (terr ? 0x10000 : 0));
+                }
             }
         }
     }
@@ -4279,7 +4058,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         s.A = sA;
         s.B = sB;
         s.PP = sPP;
-        s.Q = sQ;
         s.path = sPath;
         s.lp = sLp;
         float *boot = (float *)(smem + L::oBoot) + (wv - 1) * (L::PSx + kWave);
@@ -4400,12 +4178,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         s.A = sA;
         s.B = sB;
         s.PP = sPP;
-        s.Q = sQ;
         s.path = sPath;
         s.lp = sLp;
         float *boot = (float *)(smem + L::oBoot);
         bk_boot(s, boot, D, v_in, r_in, discount);
-        unsigned long long tl[8] = {0};
+        unsigned long long tl[4] = {0};
         stamp(tl, 3);
         int err = 0;
         long long ent_r = 0, ent_w = 0;
@@ -4425,11 +4202,6 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
                 xl[16] = (long long)(tw1[1] - ts[0]);                        // round 1: header landed
                 xl[17] = (long long)(tl[1] - tl[0]);                         // level 0 (the root)
                 xl[18] = (long long)(tw1[3] - tw1[1]);                       // round 1: pre-stage, path landed
-#ifdef MZ_DIAG_BK
-                xl[19] = (long long)(tl[4] - tl[0]);  // level 0: records + entry pass
-                xl[20] = (long long)(tl[5] - tl[0]);  // level 0: + value-set update
-                xl[21] = (long long)(tl[6] - tl[0]);  // level 0: + the node's value, q
-#endif
             }
         }
         lds_barrier();  // (2): its global stores stay in flight
@@ -4630,143 +4402,15 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
     const long long ent_r = xl[0] + xl[11] + xl[13], ent_w = xl[1] + xl[12] + xl[14];
     const int ntot = err ? tot : tot + ncl;
-    const int fc0 = uni(sB[0].x);  // the root's first child (its round-robin), read with (S1)'s records
     unsigned long long tp[4] = {0};
-    unsigned long long trep = 0;
-    (void)trep;
-    unsigned long long cal[3] = {0, 0, 0};
-    (void)cal;
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
     long long nscored = 0;
     int px = 0, pvv = 0;  // level i's node (and, by levels, its visits) in lane i; sPath past 64 levels
     if constexpr (!SEL) {
         stamp(ts, 5);
-    } else {
-#ifdef MZ_DIAG_CAL  // calibration: 16 dependent LDS reads, 64 dependent VALU ops, 64 dependent SALU ops
-        {
-            int v = l & 1;
-            const int *sI = (const int *)(smem + L::oX);
-            unsigned long long c0 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            c0 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                v = sI[v & 3];
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) :: "memory");
-                v &= 1;
-            }
-            unsigned long long c1 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int k = 0; k < 64; ++k) asm volatile("v_add_u32 %0, %0, 1" : "+v"(v));
-            unsigned long long c2 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            int sv = uni(v);
-#pragma unroll
-            for (int k = 0; k < 64; ++k) asm volatile("s_add_u32 %0, %0, 1" : "+s"(sv));
-            unsigned long long c3 = __builtin_amdgcn_s_memtime();
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            cal[0] = c1 - c0;
-            cal[1] = c2 - c1;
-            cal[2] = c3 - c2 + (unsigned long long)((sv + v) & 0);
-        }
-#endif
-        // below the 1024-node class the four waves prepare every expanded node's outcome first
-        if constexpr (!kTreeLevels<NC>) tree_select_prep<NC>(smem, 0, ntot, discount, gdelta, PS, D, tp);
+    } else if constexpr (kTreeLevels<NC>) {
         stamp(ts, 5);
-    if (!err && !kTreeLevels<NC>) {
-        // the chase: per level one LDS round trip for the node's record, structure and visits and
-        // the level's engine word; ties and the other exact cases resolved here
-        const int4 *sRec = (const int4 *)(smem + L::oCn);
-        const float2 *sTl = (const float2 *)(smem + L::oAz);
-        const int *sTc = (const int *)(smem + L::oQ);
-        cursor = uni(cursor);
-        int leaf_y = 0;
-        // the stream bounds as register values: the compiler would otherwise reload them from the
-        // parameter block every level (constant loads rematerialise under SGPR pressure)
-        int cW = gW, cPS = PS, cwo = wsh - wbase;
-        asm volatile("" : "+s"(cW), "+s"(cPS), "+s"(cwo));
-        int par_hsx = 0, nsc = 0, done = 0;
-        const int lim = cPS < kWave ? cPS : kWave;
-        const unsigned rb = lds_addr(smem) + L::oCn, tb = lds_addr(smem) + L::oAz, cb = lds_addr(smem) + L::oQ,
-                       wb = lds_addr(smem) + L::oRng;
-#ifdef MZ_DIAG_TWICE  // experiment: the chase twice over (the first discarded), to time a warm second pass
-        const int cursor0 = cursor;
-#pragma clang loop unroll(disable)
-        for (int rep = 0; rep < 2; ++rep) {
-        if (rep == 1) {
-            trep = __builtin_amdgcn_s_memtime();
-            cursor = uni(cursor0);
-            x = 0;
-            Dn = 0;
-            nscored = 0;
-            nsc = 0;
-            done = 0;
-            err = 0;
-        }
-#endif
-        while (true) {
-            chase_levels(x, Dn, cursor, nsc, par_hsx, px, pvv, done, leaf_y, l, rb, tb, cb, wb, cwo, wsh, cW, lim, fc0);
-            if (done) break;
-            // the general step
-            x = uni(x);
-            cursor = uni(cursor);
-            const int4 rec = sRec[x];  // {outcome, visits, structure word, hidden-state index}
-            const int o = cursor + cwo;
-            const bool inwin = o >= wsh && o < kRngWin;
-            const unsigned wr = sRng[inwin ? o : 0];
-            const int code = uni(rec.x), xv = uni(rec.y), y = uni(rec.z);
-            if (Dn < kWave) {
-                px = wl(px, x, Dn);
-                pvv = wl(pvv, xv, Dn);
-            } else if (l == 0) {
-                sPath[Dn] = make_int2(x, xv);
-            }
-            leaf_y = y;
-            if (code == kTreeLeaf) break;
-            const int nc = nc_of(y);
-            const bool forced = Dn == 0 && xv <= nc;  // forced root round-robin (cnode.cpp:398-399): no word
-            int next = code, consume = 1, e = 0;
-            if (forced) {
-                next = fc0 + xv - 1;
-                consume = 0;
-            } else if (code < 0) {  // ties (the word modulo the list size), one member, an empty list
-                const int fc = kSlowBase - code;
-                const int info = uni(sTc[x]);
-                const int cnt = info & 0xffff;
-                const float2 tb = sTl[x];
-                unsigned long long lst = ((unsigned long long)(unsigned)uni(f2i(tb.y)) << 32) | (unsigned)uni(f2i(tb.x));
-                if (info >> 16) e = kErrTable;
-                consume = cnt > 0 ? 1 : 0;
-                if (cnt > 1) {
-                    unsigned w = (unsigned)uni((int)wr);
-                    if (!inwin && cursor < cW) w = (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
-                    for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
-                }
-                next = fc + (cnt ? uni(__builtin_ctzll(lst)) : 0);
-            }
-            if (!e && consume && cursor >= cW) e = kErrRng;
-            if (!e && Dn + 1 >= cPS) e = kErrPath;
-            if (e) {
-                err |= e;
-                break;
-            }
-            nscored += forced ? 0 : nc;
-            cursor += consume;
-            par_hsx = uni(rec.w);
-            x = next;
-            ++Dn;
-        }
-#ifdef MZ_DIAG_TWICE
-        }
-#endif
-        nscored += nsc;
-        if (Dn == 0) err |= kErrRoot;
-        out_idx = Dn == 0 ? uni(sB[0].w) : par_hsx;  // parent->hidden_state_index_x
-        out_act = act_of(leaf_y);                      // children_action of the last edge
-    }
-    if (!err && kTreeLevels<NC>) {
+    if (!err) {
         cursor = uni(cursor);
         const bool mm_on = mm_cnt > 0;
         float den = 0.f;
@@ -4877,6 +4521,79 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         out_idx = (Dn == 0) ? uni(sB[0].w) : par_hsx;  // parent->hidden_state_index_x
         out_act = act_of(uni(xb.y));                   // children_action of the last edge
     }
+        stamp(tp, 3);
+    } else {
+        // every node's select_child outcome by the four waves (tree_select_prep), then the chase
+        tree_select_prep<NC>(smem, 0, ntot, discount, gdelta, PS, D, tp);
+        stamp(ts, 5);
+    if (!err) {
+        const int *nxt = (const int *)(smem + L::oPar);
+        const float2 *rec = (const float2 *)(smem + L::oAz);
+        cursor = uni(cursor);
+        int v, xprev = 0;
+        {
+            const int4 r0b = uni4(sB[0]);
+            const int rv = uni(sA[0].x) + 1;  // the root is on every path
+            const int nc0 = nc_of(r0b.y);
+            if (nc0 == 0) {
+                v = kTreeLeaf;
+            } else if (rv <= nc0) {
+                v = r0b.x + rv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
+            } else {
+                v = uni(nxt[0]);
+                if (v >= 0) ++cursor;
+            }
+        }
+        while (true) {
+            v = uni(v);
+            cursor = uni(cursor);
+            if (v < 0) {
+                if (v == kTreeLeaf) break;
+                // the exact record: ties (engine word modulo the list size), an empty list (child
+                // 0, no word) or a table error
+                const int xfl = uni(f2i(sQ[x]));
+                if (uni(xfl >> 16)) {
+                    err |= kErrTable;
+                    break;
+                }
+                const int cnt = uni(xfl & 0xffff);
+                int ci = 0;
+                if (cnt > 0) {
+                    const float2 rb = rec[x];
+                    unsigned long long lst = ((unsigned long long)(unsigned)uni(f2i(rb.y)) << 32) |
+                                             (unsigned)uni(f2i(rb.x));
+                    if (cursor >= gW) {
+                        err |= kErrRng;
+                        break;
+                    }
+                    if (cnt > 1) {
+                        const int o = cursor - wbase + wsh;
+                        const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                                                                   : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                        for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
+                    }
+                    ++cursor;
+                    ci = uni(__builtin_ctzll(lst));
+                }
+                v = uni(uni(sB[x].x) + ci);
+            }
+            if (Dn + 1 >= PS) {
+                err |= kErrPath;
+                break;
+            }
+            xprev = x;
+            x = v;
+            ++Dn;
+            if (Dn < kWave) px = wl(px, x, Dn);
+            else if (l == 0) sPath[Dn] = make_int2(x, 0);
+            v = uni(nxt[x]);
+            if (v >= 0) ++cursor;
+        }
+        if (cursor > gW) err |= kErrRng;  // a consumed word beyond the stream
+        if (Dn == 0) err |= kErrRoot;
+        out_idx = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
+        out_act = act_of(uni(sB[x].y));            // children_action of the last edge
+    }
     }
     stamp(ts, 6);
     if (SEL && l == 0) {
@@ -4909,14 +4626,26 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         }
     }
     if (SEL && !err) {
-        // the path {node, visits at selection} for the next back-propagation, while the row's
-        // loads are in flight
+        // the path {node, visits at selection} for the next back-propagation (and the scored
+        // children), while the row's loads are in flight
+        wait_lds();
         int2 *gp = d.path() + (size_t)t * PS;
-        if (Dn >= kWave) wait_lds();
+        int nsc = 0;
         for (int i0 = 0; i0 <= Dn; i0 += kWave) {
             const int i = i0 + l;
-            if (i <= Dn) gp[i] = (i < kWave) ? make_int2(px, pvv) : sPath[i];
+            if (i <= Dn) {
+                const int xi_ = (i < kWave) ? px : sPath[i].x;
+                if constexpr (kTreeLevels<NC>) {
+                    gp[i] = (i < kWave) ? make_int2(xi_, pvv) : sPath[i];
+                } else {
+                    const int vis = sA[xi_].x + (sFl[xi_] ? 1 : 0);
+                    gp[i] = make_int2(xi_, vis);
+                    const int nci = nc_of(sB[xi_].y);
+                    if (i < Dn && !(i == 0 && vis <= nci)) nsc += nci;  // scored levels
+                }
+            }
         }
+        if constexpr (!kTreeLevels<NC>) nscored = wave_sum(nsc);
     }
     stamp(ts, 7);
     {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
@@ -4965,10 +4694,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             case MZ_S_CYC_STAGE2: add = (long long)(ts[2] - ts[1]); break;    // barrier (1) wait
             case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;    // draws + children
             case MZ_S_CYC_BACKUP: add = (long long)(ts[4] - ts[3]); break;    // barrier (2) wait
-            case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;    // (S1), (S2), barriers (3), (4)
+            case MZ_S_CYC_MINMAX: add = (long long)(ts[5] - ts[4]); break;    // scores + tie lists (4 waves)
             case MZ_S_CYC_STAGE1: add = MZ_STAMPS ? xl[15] : 0; break;       // wave 1: bootstrap
-            case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;    // path record write
-            case MZ_S_CYC_EPILOGUE: add = (long long)(ts[8] - ts[7]); break;  // header, the row's wait + copy
+            case MZ_S_CYC_GATHER: add = (long long)(ts[7] - ts[6]); break;
+            case MZ_S_CYC_EPILOGUE: add = MZ_STAMPS ? xl[18] : 0; break;     // wave 1: pre-stage + path wait
             case MZ_S_STAMPED: add = 1; break;
             case MZ_S_CYC_W1_BACKUP: add = MZ_STAMPS ? xl[2] : 0; break;      // wave 1: its path levels
             case MZ_S_CYC_EXP_CDF: add = MZ_STAMPS ? xl[16] : 0; break;      // wave 1: header landed
@@ -4978,25 +4707,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             case MZ_S_CYC_W1_STAGE2: add = MZ_STAMPS ? xl[4] : 0; break;      // wave 2: arrival at (1)
             case MZ_S_CYC_BAK_NODES: add = MZ_STAMPS ? xl[5] : 0; break;      // wave 3: arrival at (1)
             case MZ_S_CYC_W1_ROUND1: add = MZ_STAMPS ? xl[6] : 0; break;      // wave 2: its path levels
-            case MZ_S_CYC_W1_SYNC: add = tp[0] ? (long long)(tp[1] - tp[0]) : 0; break;  // barrier (3), (S2)
-            case MZ_S_CYC_SELECT: add = (long long)(ts[6] - ts[5]); break;                // the chase / walk
-            case MZ_S_CYC_BAK_WAIT: add = tp[0] ? (long long)(tp[0] - ts[4]) : 0; break;  // (S1)
+            case MZ_S_CYC_W1_SYNC: add = MZ_STAMPS ? xl[7] : 0; break;        // wave 3: its path levels
+            case MZ_S_CYC_SELECT: add = MZ_STAMPS ? xl[8] : 0; break;         // wave 2: all after (1)
+            case MZ_S_CYC_BAK_WAIT: add = MZ_STAMPS ? xl[9] : 0; break;       // wave 3: all after (1)
             default: break;
         }
-#ifdef MZ_DIAG_CAL
-        if (l == MZ_S_CYC_STAGE1) add = (long long)cal[0];
-        if (l == MZ_S_CYC_STAGE2) add = (long long)cal[1];
-        if (l == MZ_S_CYC_W1_STAGE2) add = (long long)cal[2];
-#endif
-#ifdef MZ_DIAG_TWICE  // the chase's first and second pass
-        if (l == MZ_S_CYC_STAGE1) add = trep ? (long long)(trep - ts[5]) : 0;
-        if (l == MZ_S_CYC_STAGE2) add = trep ? (long long)(ts[6] - trep) : 0;
-#endif
-#ifdef MZ_DIAG_BK  // level 0 of wave 1's back-propagation, cumulative
-        if (l == MZ_S_CYC_STAGE2) add = xl[19];
-        if (l == MZ_S_CYC_W1_STAGE2) add = xl[20];
-        if (l == MZ_S_CYC_BAK_NODES) add = xl[21];
-#endif
         st[l] = st_old + add;
     }
     if (l == 0 && err) atomicOr(d.err(), err);
