@@ -2993,12 +2993,8 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
 //    whatever the draw), and the statistics counters.
 // Every error and output is decided from the same scalar inputs as k_chain: results are bit-identical.
 //
-// Launch arguments.  The first 14 dwords arrive preloaded in SGPRs (16 user SGPRs, 2 of them the
-// kernel-argument pointer); they hold everything waves 0 and 1 address in round 1 (the node arrays
-// lead the arena, so their offsets follow from B and P: arena_nodes).  The gather wave's source
-// rows (the host folds hsx * pool_stride into row_src) follow at once: the prologue loads them
-// from the argument segment, and wave 2 issues its row loads after that one short scalar load
-// instead of after its header round trip.
+// Launch arguments.  The first 14 dwords arrive preloaded in SGPRs; they hold everything round 1
+// addresses (the node arrays lead the arena, so their offsets follow from B and P: arena_nodes).
 // The outputs (ChainIO) are read through the kernel-argument
 // pointer by the waves that need them, where they need them: the compiler would otherwise load
 // every argument in the common prologue and wait there.  Round 1's scalar loads are issued by
@@ -3010,18 +3006,15 @@ struct ChainIO {
     long long pool_stride, row_bytes;
     char *gather_out;
     int *idx_x, *idy, *act;
-    float discount;
-    int pad;
 };
 struct Chain3Args {  // k_chain3's parameter list, for the kernel-argument offset of ChainIO
     char *base;
     const float *policy, *beta, *reward, *value;
-    int ppk, bak, hsx, row_bytes;  // (row_bytes: the gather classes' rows, <= 16 KiB)
-    const char *row_src;           // pool + hsx * pool_stride: this launch's leaf's rows, for the gather wave
+    int ppk, bak, hsx;
+    float discount;
     ChainIO io;
 };
-static_assert(offsetof(Chain3Args, row_src) == 56 && offsetof(Chain3Args, io) == 64 && sizeof(ChainIO) == 64,
-              "k_chain3 argument layout");
+static_assert(offsetof(Chain3Args, io) == 56 && sizeof(ChainIO) == 56, "k_chain3 argument layout");
 #ifdef __HIP_DEVICE_COMPILE__
 typedef const __attribute__((address_space(4))) ChainIO cChainIO;
 #else
@@ -3083,8 +3076,8 @@ int chain3_lds_bytes(int nc) { return Chain3Layout<0>(nc).total; }
 // <= 4 KiB (registers), 2 aligned rows of <= 16 KiB (LDS-DMA), 3 no gather (no pool, or no selection)
 template <int NC, bool SEL, int ROW>
 __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy, const float *beta, const float *reward,
-                                                const float *value, int ppk, int bak, int hsx, int row_bytes32,
-                                                const char *row_src, ChainIO io) {
+                                                const float *value, int ppk, int bak, int hsx, float discount,
+                                                ChainIO io) {
     static_assert(NC >= kWave && NC % kWave == 0, "k_chain3 node classes are whole waves");
     (void)io;  // (read through the kernel-argument pointer, see above)
     constexpr int NCH = NC / kWave;  // node chunks of one wave
@@ -3120,7 +3113,6 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         int8v hv = sload8(hp);  // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf
         int r_i = sload1(reward + t), v_i = sload1(value + t);
         int o_lp = sload1(&pl->d.o_lp);
-        int disc_i = sload1((const char *)iop + offsetof(ChainIO, discount));
         int4 a4[NCH];
         float2 cw[NCH];
         float pp[NCH], lpv[NCH];
@@ -3153,8 +3145,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                 pp[c] = d.PP()[nb + i];
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(hv), "+s"(r_i), "+s"(v_i), "+s"(o_lp), "+s"(disc_i)::"memory");
-        const float discount = i2f(disc_i);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(hv), "+s"(r_i), "+s"(v_i), "+s"(o_lp)::"memory");
         const float *lpt = (const float *)(base + (size_t)(unsigned)o_lp * 256);
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
@@ -3260,25 +3251,6 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         // Straight-line code in issue order (the row class ROW is a template argument): every wait
         // the compiler places then counts exactly the loads issued after the one it needs.
         // (one scalar round trip: the outputs' kernel arguments, the header, the handle's constants)
-        // the row of this launch's leaf (hidden_state_index_x = hsx), issued first: only the
-        // prologue's load of row_src ahead of it
-        const long long o = (long long)l * 16;
-        unsigned char *sbig = smem + L.total;  // (ROW 2: 16 KiB past the layout)
-        int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
-        {
-            const char *rsrc = (const char *)(const gchar *)row_src + (long long)t * row_bytes32;
-            const long long rlast = (long long)row_bytes32 - 16;
-            if constexpr (ROW == 1) {  // up to 4 KiB: four 16-byte registers per lane, offsets clamped into the row
-                gv0 = *(const int4 *)(rsrc + (o < rlast ? o : rlast));
-                gv1 = *(const int4 *)(rsrc + (o + 1024 < rlast ? o + 1024 : rlast));
-                gv2 = *(const int4 *)(rsrc + (o + 2048 < rlast ? o + 2048 : rlast));
-                gv3 = *(const int4 *)(rsrc + (o + 3072 < rlast ? o + 3072 : rlast));
-            } else if constexpr (ROW == 2) {  // up to 16 KiB: sixteen LDS-DMA chunks of 1 KiB
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    glds16a(rsrc + (o + 1024 * k < rlast ? o + 1024 * k : rlast), sbig + 1024 * k);
-            }
-        }
         int8v io8 = sload8((const void *)iop);  // pool, pool_stride, row_bytes, gather_out
         int8v hv = sload8(hp);                  // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf
         int rv0 = sload1(&d.A()[nb].x), omri = sload1(&pl->g.one_minus_rho), osti = sload1(&pl->d.o_stats);
@@ -3292,7 +3264,20 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         const int toth = hv[1], D = hv[2], herr = hv[3], leafh = hv[7];
         const int root_vis0 = rv0;
         const float omr = i2f(omri);
-        const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;  // (ROW 0)
+        // the row of this launch's leaf (hidden_state_index_x = hsx), issued first
+        const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
+        const long long last = row_bytes - 16, o = (long long)l * 16;
+        unsigned char *sbig = smem + L.total;  // (ROW 2: 16 KiB past the layout)
+        int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+        if constexpr (ROW == 1) {  // up to 4 KiB: four 16-byte registers per lane, offsets clamped into the row
+            gv0 = *(const int4 *)(src + (o < last ? o : last));
+            gv1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
+            gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
+            gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
+        } else if constexpr (ROW == 2) {  // up to 16 KiB: sixteen LDS-DMA chunks of 1 KiB
+#pragma unroll
+            for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
+        }
         d.o_stats = (unsigned)osti;
         long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
         const long long st_old = st[l < MZ_S_CYC_HEADER ? l : 0];
@@ -3362,7 +3347,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
     int r_i = sload1(reward + t), v_i = sload1(value + t);
     int4v lb = sload4(&d.Bn()[nb + Dp]);
     int4v io_xy = sload4((const char *)iop + offsetof(ChainIO, idx_x));  // idx_x, idy
-    int4v io_a = sload4((const char *)iop + offsetof(ChainIO, act));  // act, discount
+    int2v io_a = sload2((const char *)iop + offsetof(ChainIO, act));
     int omri = sload1(&pl->g.one_minus_rho), gWi = sload1(&pl->g.W), oRi = sload1(&pl->d.o_R);
     const float pol = policy[(size_t)t * A + (l < A ? l : 0)];
     const float bet = beta[(size_t)t * A + (l < A ? l : 0)];
@@ -3383,7 +3368,6 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
     const float r_in = i2f(r_i), v_in = i2f(v_i);
     int *const idx_x = (int *)(gchar *)u64_of(io_xy[0], io_xy[1]), *const idy = (int *)(gchar *)u64_of(io_xy[2], io_xy[3]);
     int *const act = (int *)(gchar *)u64_of(io_a[0], io_a[1]);
-    const float discount = i2f(io_a[2]);
     int4 leaf_b = make_int4(lb.x, lb.y, lb.z, lb.w);
     TreeHdr h;
     h.cursor = hv[0];
@@ -5040,16 +5024,13 @@ template <int NC, bool SEL, int ROW>
 void launch_chain3_row(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
     const Dev &dv = b->dev;
-    // (the first 14 argument dwords, through row_bytes, arrive preloaded in SGPRs)
-    const ChainIO io{a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act, a.discount, 0};
-    // the gather wave's rows: ROW 1 / 2 read row_bytes (<= 16 KiB) at row_src + t * row_bytes
-    const char *row_src = (ROW == 1 || ROW == 2) ? a.pool + (long long)a.hsx * a.pool_stride : nullptr;
-    const int row_bytes32 = (ROW == 1 || ROW == 2) ? (int)a.row_bytes : 0;
+    // (the first 14 argument dwords, through the discount, arrive preloaded in SGPRs)
+    const ChainIO io{a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act};
     hipLaunchKernelGGL((k_chain3<NC, SEL, ROW>), dim3(g.B), dim3(3 * kWave),
                        chain3_lds_bytes(NC) + (ROW == 2 ? 16 * 16 * kWave : 0), b->stream, (char *)dv.base, a.policy,
                        a.beta, a.reward, a.value, g.P | (g.PS << 16),
-                       (int)((unsigned)g.B | ((unsigned)g.A << 24) | ((unsigned)b->fast_ok << 31)), a.hsx, row_bytes32,
-                       row_src, io);
+                       (int)((unsigned)g.B | ((unsigned)g.A << 24) | ((unsigned)b->fast_ok << 31)), a.hsx, a.discount,
+                       io);
 }
 // the row class of a launch (k_chain3's ROW)
 int chain3_row(const StepArgs &a, bool sel) {
