@@ -3564,8 +3564,10 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
 // expansion / back-propagation / prior scores.  The engine-word draws of the expansion need no
 // staged record and run before the first.
 // --------------------------------------------------------------------------------------------
-constexpr int kBk = 3;                               // back-propagation waves of k_tree
-constexpr int kBkCap = (kRegCap / (2 * kBk)) & ~1;  // value entries per staging slot (two per wave)
+constexpr int kBk = 4;       // back-propagation waves of k_tree (waves 1 .. kBk; wave 0 expands)
+constexpr int kTreeWaves = kBk + 1;
+constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
+constexpr int kTreeReg = (2 * kBk * kBkCap > kRegCap) ? 2 * kBk * kBkCap : kRegCap;  // k_tree's staging int2s
 
 template <int NC>
 struct TreeLayout {
@@ -3583,8 +3585,8 @@ struct TreeLayout {
     static constexpr int oLp = oPath + r16(8 * (PSx + kWave));     // f32 lambda powers
     static constexpr int oRng = oLp + r16(4 * (PSx + 1 + kWave));  // u32 [kRngWin] engine words
     static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 [kBk][PSx + 64] bootstrap values
-    static constexpr int oReg = oBoot + r16(4 * kBk * (PSx + kWave));  // int2 [kRegCap] value entries; big leaf rows
-    static constexpr int oX = oReg + r16(8 * kRegCap);             // exchange between the waves
+    static constexpr int oReg = oBoot + r16(4 * kBk * (PSx + kWave));  // int2 [kTreeReg] value entries; big leaf rows
+    static constexpr int oX = oReg + r16(8 * kTreeReg);            // exchange between the waves
     static constexpr int oW = oX + r16(256);                       // f32 [64] sampling weights
     static constexpr int oP = oW + r16(4 * kWave);                 // f64 [64] probabilities, then the CDF
     static constexpr int oU = oP + r16(8 * kWave);                 // f64 [64] the draws' canonical doubles
@@ -3609,7 +3611,7 @@ int tree_lds_bytes(int nc) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_tree's back-propagation on three waves: path level i belongs to wave 1 + i % 3 (kBk waves).
+// k_tree's back-propagation on four waves: path level i belongs to wave 1 + i % 4 (kBk waves).
 // A wave stages the value entries of its first two levels before barrier (1), from path records it
 // reads with scalar loads (every entry of the node: stage_regions' need test reads structure records
 // that land only at barrier (1)); a third or later level is staged after the previous one is done.
@@ -3873,9 +3875,9 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
     float2 *sAz = (float2 *)(smem + L::oAz);
     const float *xf = (const float *)(smem + L::oX);
     const int *xi = (const int *)(smem + L::oX);
-    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), unif(xf[4]));
-    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), unif(xf[5]));
-    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
+    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), fminf(unif(xf[4]), unif(xf[6])));
+    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), fmaxf(unif(xf[5]), unif(xf[7])));
+    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]) + uni(xi[37]);  // path nodes 1..D: visited now
     const bool mm_on = mm_cnt > 0;
     float den = 0.f;
     if (mm_on) {
@@ -3951,7 +3953,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
-__global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, const float *beta, int P, int PS,
+__global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const float *policy, const float *beta, int P, int PS,
                                               int BA, int pk, int hsx, int K, float discount, int fast_ok,
                                               const float *reward, const float *value, const char *pool,
                                               long long pool_stride, long long row_bytes, char *gather_out,
@@ -3986,7 +3988,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     long long *xl = (long long *)(smem + L::oX + 64);
     const int t = blockIdx.x;
     const int l = threadIdx.x & (kWave - 1);
-    const int wv = uni((int)(threadIdx.x >> 6));
+    // wave roles: 0 expands, 1 .. 4 back-propagate (2 and 3 also stage).  Five waves on four SIMDs:
+    // one SIMD holds two, so the lightest roles, 3 and 4, get hardware waves 0 and 4 (wave w on SIMD
+    // w % 4); role 4 ends at barrier (2), before the scores and tie lists of roles 0 .. 3
+    const int hw = (int)(threadIdx.x >> 6);
+    const int wv = uni(hw == 0 ? 3 : (hw == 4 ? 4 : hw - 1));
     const size_t nb = (size_t)t * P;
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
@@ -3994,9 +4000,10 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     const cTreeHdr *hp0 = (const cTreeHdr *)(d.hdr() + t);
     const cParams *pl = (const cParams *)__builtin_assume_aligned(base, 256);
 
-    if (wv == 2 || wv == 3) {
-        // ======== waves 2, 3: stage the node records; back-propagate their path levels; then the
-        // prior scores after the back-propagation and the min/max over the visited nodes off the path ========
+    if (wv >= 2) {
+        // ======== waves 2 .. kBk: stage the node records (waves 2, 3); back-propagate their path
+        // levels; then the prior scores after the back-propagation and the min/max over the visited
+        // nodes off the path ========
         int2 bp0, bp1;
         bk_path_records(d, t, PS, wv - 1, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
@@ -4005,7 +4012,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         if (wv == 2) {
             dma_dwords(d.A() + nb, lds_addr(smem) + L::oA, 4 * ne, true);
             dma_dwords(d.Bn() + nb, lds_addr(smem) + L::oB, 4 * ne, true);
-        } else {
+        } else if (wv == 3) {
             dma_dwords(d.PP() + nb, lds_addr(smem) + L::oPP, ne, al);
             dma_dwords(d.Q() + nb, lds_addr(smem) + L::oQ, ne, al);
             dma_dwords(d.Par() + nb, lds_addr(smem) + L::oPar, ne, al);
@@ -4040,7 +4047,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
                         glds16a(d.A() + nb + i0 + l, sA + i0);
                         glds16a(d.Bn() + nb + i0 + l, sB + i0);
                         glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);  // (wave 0 stages ne)
-                    } else {
+                    } else if (wv == 3) {
                         glds4a(d.PP() + nb + i0 + l, sPP + i0);
                         glds4a(d.Q() + nb + i0 + l, sQ + i0);
                         glds4a(d.Par() + nb + i0 + l, sPar + i0);
@@ -4068,10 +4075,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, wv - 1, berr, ber, bew, bmn, bmx);
         stamp(ts, 3);
-        // nodes 1 .. tot-1 in 64-node blocks, alternating between the two waves; wave 3 takes blocks
-        // 0, 2, .. (the odd block count's extra one): its path levels (2, 5, ..) are shallower work
-        // than wave 2's (1, 4, ..)
-        constexpr int NBW = (NC + 2 * kWave - 1) / (2 * kWave);
+        // nodes 1 .. tot-1 in 64-node blocks dealt round-robin over waves 2 .. kBk, the deepest
+        // path levels' wave first: wave kBk takes blocks 0, kBk - 1, .. (its levels, kBk - 1, ..,
+        // are the shallowest work), wave 2 (levels 1, kBk + 1, ..) the last of each round
+        constexpr int NPW = kBk - 1;
+        constexpr int NBW = (NC + NPW * kWave - 1) / (NPW * kWave);
         const float *T = d.T();
         (void)T;
         float pbc[NBW];
@@ -4079,7 +4087,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         int cv = 0;
 #pragma unroll
         for (int k = 0; k < NBW; ++k) {
-            const int n = (2 * k + 3 - wv) * kWave + l;
+            const int n = (NPW * k + kBk - wv) * kWave + l;
             pbc[k] = 0.f;
             if (n >= 1 && n < tot) {
                 const int4 a = sA[n];
@@ -4106,7 +4114,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         if constexpr (SEL) {
 #pragma unroll
             for (int k = 0; k < NBW; ++k) {
-                const int n = (2 * k + 3 - wv) * kWave + l;
+                const int n = (NPW * k + kBk - wv) * kWave + l;
                 if (n >= 1 && n < tot) sPS[n] = pbc[k] * i2f(sA[n].y);  // pb_c * prior (cnode.cpp:316)
             }
         }
@@ -4117,7 +4125,13 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             xf[2 * (wv - 1)] = mn;
             xf[2 * (wv - 1) + 1] = mx;
         }
-        if (l == 0) {
+        if (l == 0 && wv == 4) {  // (xi[36], xi[37]: xl[10]'s halves)
+            xi[36] = berr;
+            xi[37] = cv;
+            xl[19] = ber;
+            xl[20] = bew;
+        }
+        if (l == 0 && wv < 4) {
             xi[7 + wv] = cv;
             xi[9 + wv] = berr;  // (xi[11], xi[12])
             xl[2 * wv + 7] = ber;  // (xl[11], xl[13])
@@ -4129,8 +4143,8 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
             }
         }
         lds_barrier();  // (2)
-        if constexpr (SEL && !kTreeLevels<NC>) {
-            const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[14]);
+        if (SEL && !kTreeLevels<NC> && wv < 4) {
+            const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]) | uni(xi[14]);
             tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, gdel, PS, D);
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
@@ -4206,7 +4220,7 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
         }
         lds_barrier();  // (2): its global stores stay in flight
         if constexpr (SEL && !kTreeLevels<NC>) {
-            const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[14]);
+            const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]) | uni(xi[14]);
             tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, gdel, PS, D);
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
@@ -4396,11 +4410,11 @@ __global__ __launch_bounds__(256) void k_tree(char *base, const float *policy, c
     stamp(ts, 4);
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
-    err |= uni(xi[8]) | uni(xi[11]) | uni(xi[12]);  // the back-propagation waves
-    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), unif(xf[4]));
-    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), unif(xf[5]));
-    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]);  // path nodes 1..D are all visited now
-    const long long ent_r = xl[0] + xl[11] + xl[13], ent_w = xl[1] + xl[12] + xl[14];
+    err |= uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]);  // the back-propagation waves
+    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), fminf(unif(xf[4]), unif(xf[6])));
+    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), fmaxf(unif(xf[5]), unif(xf[7])));
+    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]) + uni(xi[37]);  // path nodes 1..D: visited now
+    const long long ent_r = xl[0] + xl[11] + xl[13] + xl[19], ent_w = xl[1] + xl[12] + xl[14] + xl[20];
     const int ntot = err ? tot : tot + ncl;
     unsigned long long tp[4] = {0};
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
@@ -5054,7 +5068,7 @@ void launch_chain3(mz_batch *b, const StepArgs &a) {
 template <int NC, bool SEL = true>
 void launch_tree(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
-    hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(4 * kWave), TreeLayout<NC>::total, b->stream,
+    hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(kTreeWaves * kWave), TreeLayout<NC>::total, b->stream,
                        (char *)b->dev.base, a.policy, a.beta, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.hsx,
                        a.K, a.discount, b->fast_ok, a.reward, a.value, a.pool, a.pool_stride, a.row_bytes,
                        a.gather_out, a.idx_x, a.idy, a.act);
