@@ -3860,6 +3860,45 @@ constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 template <int NC>
 constexpr bool kTreeLevels = (NC >= 1024);
 
+// The chase's common levels (wave 0, uniform control flow): while the current outcome v is a child
+// (a one-member list inside the table, tree_select_prep's next node) and the path stays under lim
+// levels, step to it -- path lane Dn := x -- and read its outcome, one engine word per outcome that
+// is a child.  ~18 instructions and one LDS round trip a level; stops at a leaf, an exact record
+// or the end of the path lanes, where the general step takes over.  nb: nxt's LDS byte address.
+__device__ __forceinline__ void chase_next(int &v, int &cursor, int &x, int &Dn, int &xprev, int &px, int lane,
+                                          unsigned nb, int lim) {
+    int t0, t1, va, r0;
+    asm volatile(
+        ".Lcn%=_top:\n\t"
+        "s_cmp_lt_i32 %[v], 0\n\t"
+        "s_cbranch_scc1 .Lcn%=_out\n\t"
+        "s_add_i32 %[t0], %[dn], 1\n\t"
+        "s_cmp_ge_i32 %[t0], %[lim]\n\t"
+        "s_cbranch_scc1 .Lcn%=_out\n\t"
+        "s_lshl_b32 %[t1], %[v], 2\n\t"
+        "s_add_u32 %[t1], %[t1], %[nb]\n\t"
+        "v_mov_b32 %[va], %[t1]\n\t"
+        "ds_read_b32 %[r0], %[va]\n\t"
+        "s_mov_b32 %[xp], %[x]\n\t"
+        "s_mov_b32 %[x], %[v]\n\t"
+        "s_mov_b32 %[dn], %[t0]\n\t"
+        "v_cmp_eq_u32_e32 vcc, %[dn], %[ln]\n\t"
+        "v_mov_b32 %[va], %[x]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e32 %[px], %[px], %[va], vcc\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_readfirstlane_b32 %[v], %[r0]\n\t"
+        "s_cmp_gt_i32 %[v], -1\n\t"
+        "s_cselect_b32 %[t1], 1, 0\n\t"
+        "s_add_i32 %[cur], %[cur], %[t1]\n\t"
+        "s_branch .Lcn%=_top\n"
+        ".Lcn%=_out:"
+        : [v] "+s"(v), [cur] "+s"(cursor), [x] "+s"(x), [dn] "+s"(Dn), [xp] "+s"(xprev), [px] "+v"(px),
+          [t0] "=&s"(t0), [t1] "=&s"(t1), [va] "=&v"(va), [r0] "=&v"(r0)
+        : [nb] "s"(nb), [lim] "s"(lim), [ln] "v"(lane)
+        : "vcc", "scc", "memory");
+}
+
 template <int NC>
 __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
                                                  int D, unsigned long long *tp = nullptr) {
@@ -4545,6 +4584,8 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         const float2 *rec = (const float2 *)(smem + L::oAz);
         cursor = uni(cursor);
         int v, xprev = 0;
+        const unsigned nxb = lds_addr(smem) + L::oPar;
+        const int lim = PS < kWave ? PS : kWave;
         {
             const int4 r0b = uni4(sB[0]);
             const int rv = uni(sA[0].x) + 1;  // the root is on every path
@@ -4559,6 +4600,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
             }
         }
         while (true) {
+            chase_next(v, cursor, x, Dn, xprev, px, l, nxb, lim);
             v = uni(v);
             cursor = uni(cursor);
             if (v < 0) {
