@@ -303,7 +303,13 @@ def launch_spans(spans, S, B):
     gap = t0[1:] - t1[:-1]
     wave = {f"w{k}": round(float(np.nanmean(ends[:, :, k] - start)) / 1e3, 3)
             for k in range(3) if np.isfinite(ends[:, :, k]).any()}
+    # one workgroup's own span (its start to its last recorded wave end): the mean tree against the
+    # slowest tree of each launch (the launch ends with its slowest workgroup) and the start spread
+    own = np.nanmax(ends, axis=2) - start
     return dict(clock="s_memrealtime (100 MHz)", launches=int(len(body)),
+                tree_us_mean=round(float(np.nanmean(own)) / 1e3, 3),
+                tree_us_slowest=round(float(np.nanmean(np.nanmax(own, axis=1))) / 1e3, 3),
+                start_spread_us=round(float(np.mean(start.max(axis=1) - t0)) / 1e3, 3),
                 body_us_mean=round(float(body.mean()) / 1e3, 3), body_us_median=round(float(np.median(body)) / 1e3, 3),
                 gap_us_mean=round(float(gap.mean()) / 1e3, 3), gap_us_median=round(float(np.median(gap)) / 1e3, 3),
                 period_us=round(float(t1[-1] - t0[0]) / 1e3 / len(body), 3), wave_us=wave)
