@@ -295,7 +295,9 @@ def launch_spans(spans, S, B):
     slots, trees = min(S, 256), min(B, 1024)
     buf = (C.c_ulonglong * (4 * slots * trees))()
     spans(C.cast(buf, C.c_void_p), slots, trees, 0)
-    t = np.array(buf[:], dtype=np.float64).reshape(slots, trees, 4)[1:slots] * 10.0  # ns
+    raw = np.array(buf[:], dtype=np.uint64).reshape(slots, trees, 4)[1:slots]
+    info = np.where(raw >= np.uint64(1 << 63), raw & np.uint64((1 << 48) - 1), np.uint64(0))  # k_tree: tree shapes
+    t = np.where(raw >= np.uint64(1 << 63), 0, raw).astype(np.float64) * 10.0  # ns
     start = t[:, :, 0]
     ends = np.where(t[:, :, 1:] > 0, t[:, :, 1:], np.nan)
     t0, t1 = start.min(axis=1), np.nanmax(ends, axis=(1, 2))
@@ -306,7 +308,20 @@ def launch_spans(spans, S, B):
     # one workgroup's own span (its start to its last recorded wave end): the mean tree against the
     # slowest tree of each launch (the launch ends with its slowest workgroup) and the start spread
     own = np.nanmax(ends, axis=2) - start
-    return dict(clock="s_memrealtime (100 MHz)", launches=int(len(body)),
+    shape = {}
+    if info[:, :, 2].any():  # k_tree: the trees' own spans by back-propagation depth D, the slowest tree's D
+        D = (info[:, :, 2] & np.uint64(0xffff)).astype(np.int64)
+        slow = np.nanargmax(own, axis=1)
+        shape = dict(own_us_by_D={int(k): [round(float(np.nanmean(own[D == k])) / 1e3, 3), int((D == k).sum())]
+                                  for k in np.unique(D)},
+                     slowest_tree_D=np.bincount(D[np.arange(len(slow)), slow]).tolist(),
+                     ntot_max=int(((info[:, :, 2] >> np.uint64(16)) & np.uint64(0xffff)).max()))
+        ph = info[:, :, 3]
+        if ph.any():  # wave 0's phase ends by D: barrier (1) left, barrier (2) left, chase done, end (us)
+            marks = [((ph >> np.uint64(16 * k)) & np.uint64(0xffff)).astype(np.float64) * 0.01 for k in range(3)]
+            shape["w0_phases_us_by_D"] = {int(k): [round(float(m[D == k].mean()), 3) for m in marks] +
+                                          [round(float(np.nanmean(own[D == k])) / 1e3, 3)] for k in np.unique(D)}
+    return dict(**shape,clock="s_memrealtime (100 MHz)", launches=int(len(body)),
                 tree_us_mean=round(float(np.nanmean(own)) / 1e3, 3),
                 tree_us_slowest=round(float(np.nanmean(np.nanmax(own, axis=1))) / 1e3, 3),
                 start_spread_us=round(float(np.mean(start.max(axis=1) - t0)) / 1e3, 3),

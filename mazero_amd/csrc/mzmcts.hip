@@ -356,6 +356,31 @@ __device__ __forceinline__ void span_close(int slot, unsigned long long t0) {
     (void)t0;
 #endif
 }
+// k_tree: a tree's shape in this launch and three of wave 0's phase ends (10 ns units after its
+// start, 16 bits each), beside wave 0's span (bit 63 marks both words as no time)
+__device__ __forceinline__ unsigned long long span_mark() {
+#if MZ_SPANS
+    return __builtin_amdgcn_s_memrealtime();
+#else
+    return 0;
+#endif
+}
+__device__ __forceinline__ void span_info(int slot, unsigned long long info, unsigned long long t0,
+                                          unsigned long long m1, unsigned long long m2, unsigned long long m3) {
+#if MZ_SPANS
+    const int t = blockIdx.x;
+    const unsigned long long ph = ((m1 - t0) & 0xffff) | (((m2 - t0) & 0xffff) << 16) | (((m3 - t0) & 0xffff) << 32);
+    if (lane_id() == 0 && slot >= 0 && slot < kSpanSlots && t < kSpanTrees)
+        g_span[slot][t][1] = make_ulonglong2((1ull << 63) | info, (1ull << 63) | ph);
+#else
+    (void)slot;
+    (void)info;
+    (void)t0;
+    (void)m1;
+    (void)m2;
+    (void)m3;
+#endif
+}
 // the end of another wave role (1 or 2) of the same launch
 __device__ __forceinline__ void span_end(int slot, int role) {
 #if MZ_SPANS
@@ -3860,6 +3885,16 @@ constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 template <int NC>
 constexpr bool kTreeLevels = (NC >= 1024);
 
+// Who stages the value-set scalars in round 1: wave 0 (with the path, the flags and the leaf's
+// inputs) or, for the 1024-node class, wave 4.  Same-box A/B: 3m K = 10 9.77 -> 9.64 us with wave 4;
+// the smaller classes measured no gain (3m K = 5) or a loss (3s5z K = 5, 10.47 -> 10.59 us).
+template <int NC>
+#ifdef MZ_C_W4
+constexpr bool kTreeCW4 = true;
+#else
+constexpr bool kTreeCW4 = kTreeLevels<NC>;
+#endif
+
 // The chase's common levels (wave 0, uniform control flow): while the current outcome v is a child
 // (a one-member list inside the table, tree_select_prep's next node) and the path stays under lim
 // levels, step to it -- path lane Dn := x -- and read its outcome, one engine word per outcome that
@@ -3957,6 +3992,37 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
                 float mx = -1000000.0f;  // FLOAT_MIN (utils.h:12)
                 unsigned long long lst = 0ull;
                 int cnt = 0;
+#ifndef MZ_S2_SEQ
+                if (nc <= 8) {
+                    // up to eight children: the sequential arg-max in closed form (as the level walk),
+                    // the first maximum r and every later child within epsilon of it; {s >= FLOAT_MIN}
+                    // when no score beats FLOAT_MIN.  NaN scores join no list either way, and == makes
+                    // the sign of a zero maximum irrelevant
+                    float sc[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + (u < nc ? u : 0)];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (u >= nc) sc[u] = -INFINITY;
+                    const float M = fmaxf(fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3])),
+                                          fmaxf(fmaxf(sc[4], sc[5]), fmaxf(sc[6], sc[7])));
+                    unsigned eq = 0u, ge = 0u;
+                    if (M > mx) {
+                        const float thr = M - 0.000001f;
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) {
+                            eq |= (sc[u] == M) ? (1u << u) : 0u;
+                            ge |= (sc[u] >= thr) ? (1u << u) : 0u;
+                        }
+                        ge &= ~0u << __builtin_ctz(eq);
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) ge |= (sc[u] >= mx) ? (1u << u) : 0u;
+                    }
+                    lst = ge;
+                    cnt = __builtin_popcount(ge);
+                } else
+#endif
                 for (int i0 = 0; i0 < nc; i0 += 4) {
                     float sc[4];
 #pragma unroll
@@ -4055,6 +4121,10 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
             dma_dwords(d.PP() + nb, lds_addr(smem) + L::oPP, ne, al);
             dma_dwords(d.Q() + nb, lds_addr(smem) + L::oQ, ne, al);
             dma_dwords(d.Par() + nb, lds_addr(smem) + L::oPar, ne, al);
+        } else if constexpr (kTreeCW4<NC>) {  // wave 4: the value-set scalars (kTreeCW4)
+            for (int i0 = 0; i0 < ne; i0 += kWave)
+                if (i0 + l < ne)
+                    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(d.C() + nb + i0 + l), "s"(lds_addr(smem) + (unsigned)(L::oCn + 16 * i0)) : "memory", "m0");
         }
 #ifdef MZ_ABL_LINES  // experiment: MZ_ABL_LINES x 16 extra cache lines in round 1 (value entries, discarded)
         if (wv == 2) {
@@ -4286,6 +4356,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         glds4a(&d.hdr()[t].nxt[l < kNxt ? l : 0], sNxt);
         glds4a((const int *)st + (l < 2 * MZ_S_COUNT ? l : 0), (int *)sSt);
         // the value-set scalars of the nodes (the back-propagation waves' path nodes read them)
+        if constexpr (!kTreeCW4<NC>)
         for (int i0 = 0; i0 < ne; i0 += kWave)
             if (i0 + l < ne)
                 asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(d.C() + nb + i0 + l), "s"(lds_addr(smem) + (unsigned)(L::oCn + 16 * i0)) : "memory", "m0");
@@ -4359,6 +4430,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     // and score from here on, while this wave expands
     lds_barrier();
     stamp(ts, 2);
+    const unsigned long long rm1 = span_mark();
     const float r_in = unif(xf[60]), v_in = unif(xf[61]);  // (wave 1 staged them)
     // the sampling distribution and the K draws (std::discrete_distribution, two engine words per
     // draw, cnode.cpp:243-262)
@@ -4447,6 +4519,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     stamp(ts, 3);
     lds_barrier();  // (2) back-propagation, prior scores, min/max partials and the children are in LDS
     stamp(ts, 4);
+    const unsigned long long rm2 = span_mark();
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
     err |= uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]);  // the back-propagation waves
@@ -4652,6 +4725,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     }
     }
     stamp(ts, 6);
+    const unsigned long long rm3 = span_mark();
     if (SEL && l == 0) {
         idx_x[t] = err ? 0 : out_idx;
         idy[t] = t;
@@ -4772,6 +4846,8 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     }
     if (l == 0 && err) atomicOr(d.err(), err);
     span_close(hsx, rt0);
+    span_info(hsx, (unsigned long long)(D & 0xffff) | ((unsigned long long)(ntot & 0xffff) << 16) |
+                       ((unsigned long long)(Dn & 0xffff) << 32), rt0, rm1, rm2, rm3);
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
