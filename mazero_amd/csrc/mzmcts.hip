@@ -3888,6 +3888,16 @@ constexpr bool kTreeLevels = (NC >= 1024);
 // Who stages the value-set scalars in round 1: wave 0 (with the path, the flags and the leaf's
 // inputs) or, for the 1024-node class, wave 4.  Same-box A/B: 3m K = 10 9.77 -> 9.64 us with wave 4;
 // the smaller classes measured no gain (3m K = 5) or a loss (3s5z K = 5, 10.47 -> 10.59 us).
+// Who gathers the leaf's row in the precomputed-walk classes: wave 1, after its own copy of the
+// chase (the same reads of the same LDS state), while wave 0 writes the path record, the header
+// and the counters; the level walk (1024-node class) gathers on wave 0.
+template <int NC>
+#ifdef MZ_NO_W1G
+constexpr bool kTreeW1Gather = false;
+#else
+constexpr bool kTreeW1Gather = !kTreeLevels<NC>;
+#endif
+
 template <int NC>
 #ifdef MZ_C_W4
 constexpr bool kTreeCW4 = true;
@@ -4057,6 +4067,126 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
     lds_barrier();  // (4)
 }
 
+// The chase after tree_select_prep (cnode.cpp:381-413 over the precomputed outcomes): from the root,
+// next nodes one LDS read a level (chase_next), exact records (ties: the engine word modulo the list
+// size; an empty list: child 0; table errors) in the general step.  Wave 0 records the path (REC);
+// wave 1 runs the same chase on the same LDS state for the leaf's parent only, and gathers its row.
+template <int NC, bool REC>
+__device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, int t, int gW, int wbase, int wsh,
+                                           int PS, int &cursor, int &err, int &Dn, int &x, int &xprev, int &px) {
+    using L = TreeLayout<NC>;
+    const int l = lane_id();
+    const int4 *sA = (const int4 *)(smem + L::oA);
+    const int4 *sB = (const int4 *)(smem + L::oB);
+    const float *sQ = (const float *)(smem + L::oQ);
+    int2 *sPath = (int2 *)(smem + L::oPath);
+    const unsigned *sRng = (const unsigned *)(smem + L::oRng);
+    const int *nxt = (const int *)(smem + L::oPar);
+    const float2 *rec = (const float2 *)(smem + L::oAz);
+    cursor = uni(cursor);
+    int v;
+    const unsigned nxb = lds_addr(smem) + L::oPar;
+    const int lim = PS < kWave ? PS : kWave;
+    {
+        const int4 r0b = uni4(sB[0]);
+        const int rv = uni(sA[0].x) + 1;  // the root is on every path
+        const int nc0 = nc_of(r0b.y);
+        if (nc0 == 0) {
+            v = kTreeLeaf;
+        } else if (rv <= nc0) {
+            v = r0b.x + rv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
+        } else {
+            v = uni(nxt[0]);
+            if (v >= 0) ++cursor;
+        }
+    }
+    while (true) {
+        chase_next(v, cursor, x, Dn, xprev, px, l, nxb, lim);
+        v = uni(v);
+        cursor = uni(cursor);
+        if (v < 0) {
+            if (v == kTreeLeaf) break;
+#ifndef MZ_SLOW_OLD
+            // the exact record: ties (engine word modulo the list size), an empty list (child 0, no
+            // word) or a table error.  Everything it reads depends only on x and the cursor, so all
+            // of it is one LDS round trip; the k-th listed child is one ballot (mbcnt rank)
+            const int o = cursor - wbase + wsh;
+            const bool inwin = o >= wsh && o < kRngWin;
+            const float qv = sQ[x];
+            const float2 rb = rec[x];
+            const int bx = sB[x].x;
+            const unsigned wwin = sRng[inwin ? o : 0];
+            const int xfl = uni(f2i(qv));
+            if (uni(xfl >> 16)) {
+                err |= kErrTable;
+                break;
+            }
+            const int cnt = uni(xfl & 0xffff);
+            int ci = 0;
+            if (cnt > 0) {
+                if (cursor >= gW) {
+                    err |= kErrRng;
+                    break;
+                }
+                const unsigned lo = (unsigned)uni(f2i(rb.x)), hi = (unsigned)uni(f2i(rb.y));
+                if (cnt > 1) {
+                    const unsigned w = inwin ? (unsigned)uni((int)wwin) : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                    const int k = uni((int)(w % (unsigned)cnt));
+                    const unsigned lst_l = (l < 32) ? (lo >> l) : (hi >> (l - 32));
+                    const int below = (int)__builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+                    ci = uni(__builtin_ctzll(ballot((lst_l & 1u) && below == k)));
+                } else {
+                    ci = lo ? __builtin_ctz(lo) : 32 + __builtin_ctz(hi);
+                }
+                ++cursor;
+            }
+            v = uni(uni(bx) + ci);
+#else
+            // the exact record: ties (engine word modulo the list size), an empty list (child
+            // 0, no word) or a table error
+            const int xfl = uni(f2i(sQ[x]));
+            if (uni(xfl >> 16)) {
+                err |= kErrTable;
+                break;
+            }
+            const int cnt = uni(xfl & 0xffff);
+            int ci = 0;
+            if (cnt > 0) {
+                const float2 rb = rec[x];
+                unsigned long long lst = ((unsigned long long)(unsigned)uni(f2i(rb.y)) << 32) |
+                                         (unsigned)uni(f2i(rb.x));
+                if (cursor >= gW) {
+                    err |= kErrRng;
+                    break;
+                }
+                if (cnt > 1) {
+                    const int o = cursor - wbase + wsh;
+                    const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                                                               : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                    for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
+                }
+                ++cursor;
+                ci = uni(__builtin_ctzll(lst));
+            }
+            v = uni(uni(sB[x].x) + ci);
+#endif
+        }
+        if (Dn + 1 >= PS) {
+            err |= kErrPath;
+            break;
+        }
+        xprev = x;
+        x = v;
+        ++Dn;
+        if (Dn < kWave) px = wl(px, x, Dn);
+        else if (REC && l == 0) sPath[Dn] = make_int2(x, 0);
+        v = uni(nxt[x]);
+        if (v >= 0) ++cursor;
+    }
+    if (cursor > gW) err |= kErrRng;  // a consumed word beyond the stream
+    if (Dn == 0) err |= kErrRoot;
+}
+
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
 __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const float *policy, const float *beta, int P, int PS,
                                               int BA, int pk, int hsx, int K, float discount, int fast_ok,
@@ -4067,7 +4197,10 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     // compiler's wait-count state of one role (its loads, stores and LDS-DMA) never forces waits
     // into another's code.  The barriers are the same two s_barrier in every role.
     using L = TreeLayout<NC>;
-    (void)fast_ok;
+    // fast_ok bit 1: one workgroup per CU (B <= the CU count), where wave 1 gathers the leaf's row;
+    // with two workgroups sharing a CU its copy of the chase competes for the other's SIMDs
+    // (3s5z K = 5, 512 trees: +0.5 us per launch), so wave 0 gathers there
+    const bool w1g = kTreeW1Gather<NC> && (fast_ok & 2) != 0;
     const int B = BA & 0xffffff, A = (int)((unsigned)BA >> 24);
     const int pe = pk & 0x1ffff, gK = (int)((unsigned)pk >> 17);
     const int ne = (1ll + (long long)gK * (pe - 1)) < P ? 1 + gK * (pe - 1) : P;  // node bound (launch_step)
@@ -4265,6 +4398,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         int2 bp0, bp1;
         bk_path_records(d, t, PS, 0, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
+        const int gW1 = pl->g.W;
         if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
         dma_dwords(d.lp(), lds_addr(smem) + L::oLp, PS + 1, true);
         unsigned long long tw1[4] = {0};
@@ -4329,8 +4463,36 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         }
         lds_barrier();  // (2): its global stores stay in flight
         if constexpr (SEL && !kTreeLevels<NC>) {
-            const int ncl = uni(xi[15]), e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]) | uni(xi[14]);
+            const int ncl = uni(xi[15]);
+            int e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]) | uni(xi[14]);
             tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, gdel, PS, D);
+            if (w1g && pool && !e) {
+                // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[parent's hsx][t], after
+                // this wave's copy of wave 0's chase (no path record)
+                int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0;
+                tree_chase<NC, false>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px);
+                if (!e) {
+                    const int oi = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
+                    const char *src = pool + (long long)oi * pool_stride + (long long)t * row_bytes;
+                    char *gdst = gather_out + (long long)t * row_bytes;
+                    const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool |
+                                      (long long)(uintptr_t)gather_out) & 15) == 0;
+                    if (al) {
+                        for (long long o0 = (long long)l * 16; o0 < row_bytes; o0 += 4 * 16 * kWave) {
+                            int4 v4[4];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                if (o0 + 16 * kWave * k < row_bytes) v4[k] = *(const int4 *)(src + o0 + 16 * kWave * k);
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                if (o0 + 16 * kWave * k < row_bytes) *(int4 *)(gdst + o0 + 16 * kWave * k) = v4[k];
+                        }
+                    } else {
+                        for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
+                            *(int *)(gdst + o2) = *(const int *)(src + o2);
+                    }
+                }
+            }
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
@@ -4430,7 +4592,11 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     // and score from here on, while this wave expands
     lds_barrier();
     stamp(ts, 2);
+#ifndef MZ_SPANS_EPI
     const unsigned long long rm1 = span_mark();
+#else
+    unsigned long long rm1 = 0;
+#endif
     const float r_in = unif(xf[60]), v_in = unif(xf[61]);  // (wave 1 staged them)
     // the sampling distribution and the K draws (std::discrete_distribution, two engine words per
     // draw, cnode.cpp:243-262)
@@ -4515,11 +4681,18 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     if (l == 0) {
         xi[15] = ncl;
         xi[14] = err;
+        xi[58] = cursor;  // the selection's first engine word, for wave 1's copy of the chase
+        xi[59] = wsh;
+        xi[62] = wbase;
     }
     stamp(ts, 3);
     lds_barrier();  // (2) back-propagation, prior scores, min/max partials and the children are in LDS
     stamp(ts, 4);
+#ifndef MZ_SPANS_EPI
     const unsigned long long rm2 = span_mark();
+#else
+    unsigned long long rm2 = 0;
+#endif
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
     err |= uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]);  // the back-propagation waves
@@ -4653,79 +4826,18 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         tree_select_prep<NC>(smem, 0, ntot, discount, gdelta, PS, D, tp);
         stamp(ts, 5);
     if (!err) {
-        const int *nxt = (const int *)(smem + L::oPar);
-        const float2 *rec = (const float2 *)(smem + L::oAz);
-        cursor = uni(cursor);
-        int v, xprev = 0;
-        const unsigned nxb = lds_addr(smem) + L::oPar;
-        const int lim = PS < kWave ? PS : kWave;
-        {
-            const int4 r0b = uni4(sB[0]);
-            const int rv = uni(sA[0].x) + 1;  // the root is on every path
-            const int nc0 = nc_of(r0b.y);
-            if (nc0 == 0) {
-                v = kTreeLeaf;
-            } else if (rv <= nc0) {
-                v = r0b.x + rv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
-            } else {
-                v = uni(nxt[0]);
-                if (v >= 0) ++cursor;
-            }
-        }
-        while (true) {
-            chase_next(v, cursor, x, Dn, xprev, px, l, nxb, lim);
-            v = uni(v);
-            cursor = uni(cursor);
-            if (v < 0) {
-                if (v == kTreeLeaf) break;
-                // the exact record: ties (engine word modulo the list size), an empty list (child
-                // 0, no word) or a table error
-                const int xfl = uni(f2i(sQ[x]));
-                if (uni(xfl >> 16)) {
-                    err |= kErrTable;
-                    break;
-                }
-                const int cnt = uni(xfl & 0xffff);
-                int ci = 0;
-                if (cnt > 0) {
-                    const float2 rb = rec[x];
-                    unsigned long long lst = ((unsigned long long)(unsigned)uni(f2i(rb.y)) << 32) |
-                                             (unsigned)uni(f2i(rb.x));
-                    if (cursor >= gW) {
-                        err |= kErrRng;
-                        break;
-                    }
-                    if (cnt > 1) {
-                        const int o = cursor - wbase + wsh;
-                        const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
-                                                                   : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
-                        for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
-                    }
-                    ++cursor;
-                    ci = uni(__builtin_ctzll(lst));
-                }
-                v = uni(uni(sB[x].x) + ci);
-            }
-            if (Dn + 1 >= PS) {
-                err |= kErrPath;
-                break;
-            }
-            xprev = x;
-            x = v;
-            ++Dn;
-            if (Dn < kWave) px = wl(px, x, Dn);
-            else if (l == 0) sPath[Dn] = make_int2(x, 0);
-            v = uni(nxt[x]);
-            if (v >= 0) ++cursor;
-        }
-        if (cursor > gW) err |= kErrRng;  // a consumed word beyond the stream
-        if (Dn == 0) err |= kErrRoot;
+        int xprev = 0;
+        tree_chase<NC, true>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px);
         out_idx = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
         out_act = act_of(uni(sB[x].y));            // children_action of the last edge
     }
     }
     stamp(ts, 6);
+#ifndef MZ_SPANS_EPI
     const unsigned long long rm3 = span_mark();
+#else
+    unsigned long long rm3 = 0;
+#endif
     if (SEL && l == 0) {
         idx_x[t] = err ? 0 : out_idx;
         idy[t] = t;
@@ -4737,7 +4849,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     bool gath_lds = false;
     char *gdst = nullptr;
     unsigned char *sbig = smem + L::oReg;
-    if (SEL && pool && !err) {
+    if (SEL && !w1g && pool && !err) {
         const char *src = pool + (long long)out_idx * pool_stride + (long long)t * row_bytes;
         gdst = gather_out + (long long)t * row_bytes;
         const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) &
@@ -4755,6 +4867,9 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
                 *(int *)(gdst + o2) = *(const int *)(src + o2);
         }
     }
+#ifdef MZ_SPANS_EPI
+    rm1 = span_mark();
+#endif
     if (SEL && !err) {
         // the path {node, visits at selection} for the next back-propagation (and the scored
         // children), while the row's loads are in flight
@@ -4778,6 +4893,9 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         if constexpr (!kTreeLevels<NC>) nscored = wave_sum(nsc);
     }
     stamp(ts, 7);
+#ifdef MZ_SPANS_EPI
+    rm2 = span_mark();
+#endif
     {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
         const int cur = err ? h.cursor : cursor;
         const int o0 = cur - wbase + wsh;
@@ -4805,6 +4923,9 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     }
     if (gath_lds) {
         wait_vm();
+#ifdef MZ_SPANS_EPI
+        rm3 = span_mark();
+#endif
         for (long long o = (long long)l * 16; o < row_bytes; o += 16 * kWave) *(int4 *)(gdst + o) = *(const int4 *)(sbig + o);
     }
     stamp(ts, 8);
@@ -5183,12 +5304,23 @@ void launch_chain3(mz_batch *b, const StepArgs &a) {
     }
 }
 
+static int device_cus() {  // compute units of the current device (one MI355X: 256)
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && c > 0) n = c;
+        else n = 1;
+    }
+    return n;
+}
+
 template <int NC, bool SEL = true>
 void launch_tree(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
+    const int flags = (b->fast_ok ? 1 : 0) | (g.B <= device_cus() ? 2 : 0);
     hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(kTreeWaves * kWave), TreeLayout<NC>::total, b->stream,
                        (char *)b->dev.base, a.policy, a.beta, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.hsx,
-                       a.K, a.discount, b->fast_ok, a.reward, a.value, a.pool, a.pool_stride, a.row_bytes,
+                       a.K, a.discount, flags, a.reward, a.value, a.pool, a.pool_stride, a.row_bytes,
                        a.gather_out, a.idx_x, a.idy, a.act);
 }
 

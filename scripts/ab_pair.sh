@@ -9,7 +9,7 @@ if [ -z "$SKIP_PYTEST" ]; then
   STEPS=pytest bash scripts/r3_iter.sh || exit $?
   grep -q " passed" gpurun_out/it/pytest_gpu.log && ! grep -qE "[0-9]+ (failed|error)" gpurun_out/it/pytest_gpu.log || { echo "pytest not green"; exit 1; }
 fi
-for a in ${ALT1:-variant_old} $ALT2; do
+for a in ${ALTS:-${ALT1:-variant_old} $ALT2}; do
   echo "== product vs $a"
   ALT=$B/$a.so bash scripts/ab_ktree.sh || exit $?
 done
