@@ -3589,14 +3589,30 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
 // expansion / back-propagation / prior scores.  The engine-word draws of the expansion need no
 // staged record and run before the first.
 // --------------------------------------------------------------------------------------------
-constexpr int kBk = 4;       // back-propagation waves of k_tree (waves 1 .. kBk; wave 0 expands)
-constexpr int kTreeWaves = kBk + 1;
+// back-propagation waves of k_tree (waves 1 .. kBkN; wave 0 expands): seven (eight waves, two per
+// SIMD) for pools up to 384 nodes, whose trees hold one workgroup per CU; four (five waves) for the
+// larger classes, whose LDS then still fits two workgroups per CU (3s5z: 512 trees)
+#ifndef MZ_TREE_BK
+#define MZ_TREE_BK 7
+#endif
+template <int NC>
+constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : 4;
+template <int NC>
+constexpr int kTreeWavesN = kBkN<NC> + 1;
 constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
-constexpr int kTreeReg = (2 * kBk * kBkCap > kRegCap) ? 2 * kBk * kBkCap : kRegCap;  // k_tree's staging int2s
+// per back-propagation wave, exchanged at barrier (2): its min/max partial, visited-node count,
+// error word and value-entry counters
+struct BkOut {
+    float mn, mx;
+    int cv, err;
+    long long er, ew;
+};
 
 template <int NC>
 struct TreeLayout {
     static constexpr int r16(int x) { return (x + 15) & ~15; }
+    static constexpr int BK = kBkN<NC>;
+    static constexpr int kTreeReg = (2 * BK * kBkCap > kRegCap) ? 2 * BK * kBkCap : kRegCap;  // staging int2s
     static constexpr int PSx = NC / 2 + 1;                         // PS = S + 2 <= P / K <= NC / 2
     static constexpr int oA = 0;                                   // int4 [NC] staged {visit, prior, value, reward}
     static constexpr int oB = oA + r16(16 * NC);                   // int4 [NC] staged structure records
@@ -3609,8 +3625,8 @@ struct TreeLayout {
     static constexpr int oPath = oAz + r16(8 * NC);                // int2 [PSx] the path {node, visits at selection}
     static constexpr int oLp = oPath + r16(8 * (PSx + kWave));     // f32 lambda powers
     static constexpr int oRng = oLp + r16(4 * (PSx + 1 + kWave));  // u32 [kRngWin] engine words
-    static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 [kBk][PSx + 64] bootstrap values
-    static constexpr int oReg = oBoot + r16(4 * kBk * (PSx + kWave));  // int2 [kTreeReg] value entries; big leaf rows
+    static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 [BK][PSx + 64] bootstrap values
+    static constexpr int oReg = oBoot + r16(4 * BK * (PSx + kWave));  // int2 [kTreeReg] value entries; big leaf rows
     static constexpr int oX = oReg + r16(8 * kTreeReg);            // exchange between the waves
     static constexpr int oW = oX + r16(256);                       // f32 [64] sampling weights
     static constexpr int oP = oW + r16(4 * kWave);                 // f64 [64] probabilities, then the CDF
@@ -3622,7 +3638,8 @@ struct TreeLayout {
     static constexpr int oCn = oSt + r16(8 * kWave);               // float4 [NC] staged value-set scalars
     static constexpr int oPb = oCn + r16(16 * NC);                 // f32 [PSx] logf((n + c2 + 1)/c2) + c1
     static constexpr int oSq = oPb + r16(4 * (PSx + kWave));       // f64 [PSx] sqrt(n)
-    static constexpr int total = oSq + r16(8 * (PSx + kWave));
+    static constexpr int oXB = oSq + r16(8 * (PSx + kWave));        // BkOut [BK + 1] (index = wave)
+    static constexpr int total = oXB + r16((int)sizeof(BkOut) * (BK + 1));
 };
 int tree_lds_bytes(int nc) {
     switch (nc) {
@@ -3684,13 +3701,15 @@ __device__ __forceinline__ int2 ldsc2(const int2 *p) {
 
 // the path records of wave k's first two levels (scalar loads, issued at the wave's start: indices
 // clamped into the tree's PS records, so the reads need not wait for the header's path length)
+template <int BK>
 __device__ __forceinline__ void bk_path_records(const Dev &d, int t, int PS, int k, int2 &p0, int2 &p1) {
     const int2 *gp = d.path() + (size_t)t * PS;
     p0 = ldsc2(gp + (k < PS ? k : PS - 1));
-    p1 = ldsc2(gp + (k + kBk < PS ? k + kBk : PS - 1));
+    p1 = ldsc2(gp + (k + BK < PS ? k + BK : PS - 1));
 }
 
 // their value entries -> the wave's two staging slots (every entry of the node)
+template <int BK>
 __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, int D, int k, int2 p0, int2 p1,
                                              int2 *sReg) {
     const int l = lane_id();
@@ -3698,7 +3717,7 @@ __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, 
     const int2 *gV = d.V() + (size_t)t * P * E;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-        const int i = k + kBk * j;
+        const int i = k + BK * j;
         const int2 pe = j == 0 ? p0 : p1;
         if (i > D) break;
         if (pe.x < 0 || pe.x >= P || pe.y < 0 || pe.y > kBkCap) continue;  // (staged after barrier (1))
@@ -3740,7 +3759,8 @@ __device__ __forceinline__ void bk_boot(const Lds &s, float *boot, int D, float 
     wait_lds();
 }
 
-// wave k's path levels k, k + kBk, ... (CTree::back_propagate, cnode.cpp:415-450, node by node)
+// wave k's path levels k, k + BK, ... (CTree::back_propagate, cnode.cpp:415-450, node by node)
+template <int BK>
 __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds &s, const float4 *sCn, float2 *sAz,
                                           const float *boot, int2 *sReg, BkPre pre, int t, int D, float reward,
                                           float disc, int k, int &err, long long &ent_r, long long &ent_w, float &pmn,
@@ -3751,7 +3771,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
     pmx = -INFINITY;
     wait_vm();  // the pre-staged entries (in flight across barrier (1))
     if (MZ_STAMPS && tl) tl[0] = __builtin_amdgcn_s_memtime();
-    for (int j = 0, i = k; i <= D; ++j, i += kBk) {
+    for (int j = 0, i = k; i <= D; ++j, i += BK) {
         // the level's node: from the pre-stage's scalar path records (no LDS round trip) or the path
         int n, nv;
         if (j == 0 && pre.nv0 >= 0) {
@@ -3944,6 +3964,30 @@ __device__ __forceinline__ void chase_next(int &v, int &cursor, int &x, int &Dn,
         : "vcc", "scc", "memory");
 }
 
+// the back-propagation waves' exchange records (after barrier (2)): joined error word, min/max and
+// visited-node count (path nodes 1 .. D are visited now, cnode.cpp:431-447)
+template <int NC>
+__device__ __forceinline__ int bk_err(const unsigned char *smem) {
+    const BkOut *xb = (const BkOut *)(smem + TreeLayout<NC>::oXB);
+    int e = 0;
+#pragma unroll
+    for (int j = 1; j <= kBkN<NC>; ++j) e |= uni(xb[j].err);
+    return e;
+}
+template <int NC>
+__device__ __forceinline__ void bk_minmax(const unsigned char *smem, int D, float &mn, float &mx, int &cnt) {
+    const BkOut *xb = (const BkOut *)(smem + TreeLayout<NC>::oXB);
+    mn = unif(xb[1].mn);
+    mx = unif(xb[1].mx);
+    cnt = D >= 1 ? D : 0;
+#pragma unroll
+    for (int j = 2; j <= kBkN<NC>; ++j) {
+        mn = fminf(mn, unif(xb[j].mn));
+        mx = fmaxf(mx, unif(xb[j].mx));
+        cnt += uni(xb[j].cv);
+    }
+}
+
 template <int NC>
 __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, int ntot, float disc, float gdelta, int PS,
                                                  int D, unsigned long long *tp = nullptr) {
@@ -3957,11 +4001,9 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
     float *sSc = (float *)(smem + L::oPS);
     const int *sFl = (const int *)(smem + L::oFl);
     float2 *sAz = (float2 *)(smem + L::oAz);
-    const float *xf = (const float *)(smem + L::oX);
-    const int *xi = (const int *)(smem + L::oX);
-    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), fminf(unif(xf[4]), unif(xf[6])));
-    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), fmaxf(unif(xf[5]), unif(xf[7])));
-    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]) + uni(xi[37]);  // path nodes 1..D: visited now
+    float mmn, mmx;
+    int mm_cnt;
+    bk_minmax<NC>(smem, D, mmn, mmx, mm_cnt);
     const bool mm_on = mm_cnt > 0;
     float den = 0.f;
     if (mm_on) {
@@ -4188,7 +4230,7 @@ __device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, in
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
-__global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const float *policy, const float *beta, int P, int PS,
+__global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const float *policy, const float *beta, int P, int PS,
                                               int BA, int pk, int hsx, int K, float discount, int fast_ok,
                                               const float *reward, const float *value, const char *pool,
                                               long long pool_stride, long long row_bytes, char *gather_out,
@@ -4229,8 +4271,13 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     // wave roles: 0 expands, 1 .. 4 back-propagate (2 and 3 also stage).  Five waves on four SIMDs:
     // one SIMD holds two, so the lightest roles, 3 and 4, get hardware waves 0 and 4 (wave w on SIMD
     // w % 4); role 4 ends at barrier (2), before the scores and tie lists of roles 0 .. 3
+    // (eight waves: hardware waves w and w + 4 share SIMD w % 4; roles 0 .. 3 -- the expansion, the
+    // root, path levels 1 and 2 -- get one SIMD each, paired with the roles of the deepest levels 6,
+    // 5, 4, 3, which also take the prior-score blocks)
+    constexpr int BK = kBkN<NC>;
     const int hw = (int)(threadIdx.x >> 6);
-    const int wv = uni(hw == 0 ? 3 : (hw == 4 ? 4 : hw - 1));
+    const int wv = uni(BK == 4 ? (hw == 0 ? 3 : (hw == 4 ? 4 : hw - 1)) : (hw < 4 ? hw : BK + 4 - hw));
+    BkOut *xbo = (BkOut *)(smem + L::oXB);
     const size_t nb = (size_t)t * P;
     unsigned long long ts[10] = {0};
     stamp(ts, 0);
@@ -4243,7 +4290,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         // levels; then the prior scores after the back-propagation and the min/max over the visited
         // nodes off the path ========
         int2 bp0, bp1;
-        bk_path_records(d, t, PS, wv - 1, bp0, bp1);
+        bk_path_records<BK>(d, t, PS, wv - 1, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
         if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
         const bool al = (P & 3) == 0;  // the tree's 4-byte arrays start 16-byte aligned
@@ -4254,7 +4301,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
             dma_dwords(d.PP() + nb, lds_addr(smem) + L::oPP, ne, al);
             dma_dwords(d.Q() + nb, lds_addr(smem) + L::oQ, ne, al);
             dma_dwords(d.Par() + nb, lds_addr(smem) + L::oPar, ne, al);
-        } else if constexpr (kTreeCW4<NC>) {  // wave 4: the value-set scalars (kTreeCW4)
+        } else if (kTreeCW4<NC> && wv == 4) {  // wave 4: the value-set scalars (kTreeCW4)
             for (int i0 = 0; i0 < ne; i0 += kWave)
                 if (i0 + l < ne)
                     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(d.C() + nb + i0 + l), "s"(lds_addr(smem) + (unsigned)(L::oCn + 16 * i0)) : "memory", "m0");
@@ -4296,7 +4343,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
                     }
                 }
         // this wave's path levels' value entries: issued last, in flight across barrier (1)
-        const BkPre pre = bk_prestage(d, t, P, g.E, D, wv - 1, bp0, bp1, (int2 *)(smem + L::oReg));
+        const BkPre pre = bk_prestage<BK>(d, t, P, g.E, D, wv - 1, bp0, bp1, (int2 *)(smem + L::oReg));
         wait_vm_but(pre.ndma);
         stamp(ts, 1);
         lds_barrier();  // (1)
@@ -4314,13 +4361,13 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         int berr = 0;
         long long ber = 0, bew = 0;
         float bmn, bmx;
-        bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+        bk_levels<BK>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, wv - 1, berr, ber, bew, bmn, bmx);
         stamp(ts, 3);
         // nodes 1 .. tot-1 in 64-node blocks dealt round-robin over waves 2 .. kBk, the deepest
         // path levels' wave first: wave kBk takes blocks 0, kBk - 1, .. (its levels, kBk - 1, ..,
         // are the shallowest work), wave 2 (levels 1, kBk + 1, ..) the last of each round
-        constexpr int NPW = kBk - 1;
+        constexpr int NPW = BK - 1;
         constexpr int NBW = (NC + NPW * kWave - 1) / (NPW * kWave);
         const float *T = d.T();
         (void)T;
@@ -4329,7 +4376,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         int cv = 0;
 #pragma unroll
         for (int k = 0; k < NBW; ++k) {
-            const int n = (NPW * k + kBk - wv) * kWave + l;
+            const int n = (NPW * k + BK - wv) * kWave + l;
             pbc[k] = 0.f;
             if (n >= 1 && n < tot) {
                 const int4 a = sA[n];
@@ -4356,7 +4403,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         if constexpr (SEL) {
 #pragma unroll
             for (int k = 0; k < NBW; ++k) {
-                const int n = (NPW * k + kBk - wv) * kWave + l;
+                const int n = (NPW * k + BK - wv) * kWave + l;
                 if (n >= 1 && n < tot) sPS[n] = pbc[k] * i2f(sA[n].y);  // pb_c * prior (cnode.cpp:316)
             }
         }
@@ -4364,20 +4411,16 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         mn = fminf(wave_min_to63(mn), bmn);  // (with this wave's path nodes)
         mx = fmaxf(wave_max_to63(mx), bmx);
         if (l == 63) {
-            xf[2 * (wv - 1)] = mn;
-            xf[2 * (wv - 1) + 1] = mx;
+            xbo[wv].mn = mn;
+            xbo[wv].mx = mx;
         }
-        if (l == 0 && wv == 4) {  // (xi[36], xi[37]: xl[10]'s halves)
-            xi[36] = berr;
-            xi[37] = cv;
-            xl[19] = ber;
-            xl[20] = bew;
+        if (l == 0) {
+            xbo[wv].cv = cv;
+            xbo[wv].err = berr;
+            xbo[wv].er = ber;
+            xbo[wv].ew = bew;
         }
         if (l == 0 && wv < 4) {
-            xi[7 + wv] = cv;
-            xi[9 + wv] = berr;  // (xi[11], xi[12])
-            xl[2 * wv + 7] = ber;  // (xl[11], xl[13])
-            xl[2 * wv + 8] = bew;  // (xl[12], xl[14])
             if (MZ_STAMPS) {
                 xl[wv + 2] = (long long)(ts[1] - ts[0]);  // (xl[4], xl[5]) arrival at barrier (1)
                 xl[wv + 4] = (long long)(ts[3] - ts[2]);  // (xl[6], xl[7]) its path levels
@@ -4386,7 +4429,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         }
         lds_barrier();  // (2)
         if (SEL && !kTreeLevels<NC> && wv < 4) {
-            const int ncl = uni(xi[15]), err = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]) | uni(xi[14]);
+            const int ncl = uni(xi[15]), err = bk_err<NC>(smem) | uni(xi[14]);
             tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, gdel, PS, D);
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
@@ -4396,7 +4439,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
     if (wv == 1) {
         // ======== wave 1: CTree::back_propagate (cnode.cpp:415-450) of its levels ========
         int2 bp0, bp1;
-        bk_path_records(d, t, PS, 0, bp0, bp1);
+        bk_path_records<BK>(d, t, PS, 0, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
         const int gW1 = pl->g.W;
         if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
@@ -4423,7 +4466,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
             return;
         }
         stamp(tw1, 1);
-        const BkPre pre = bk_prestage(d, t, P, g.E, D, 0, bp0, bp1, (int2 *)(smem + L::oReg));
+        const BkPre pre = bk_prestage<BK>(d, t, P, g.E, D, 0, bp0, bp1, (int2 *)(smem + L::oReg));
         stamp(tw1, 2);
         wait_vm_but(pre.ndma);  // the lambda powers, reward and value (the entries stay in flight)
         stamp(tw1, 3);
@@ -4444,14 +4487,15 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         int err = 0;
         long long ent_r = 0, ent_w = 0;
         float pmn, pmx;
-        bk_levels(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+        bk_levels<BK>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, 0, err, ent_r, ent_w, pmn, pmx, tl);
         if (l == 0) {
-            xf[0] = pmn;
-            xf[1] = pmx;
-            xi[8] = err;
-            xl[0] = ent_r;
-            xl[1] = ent_w;
+            xbo[1].mn = pmn;
+            xbo[1].mx = pmx;
+            xbo[1].cv = 0;
+            xbo[1].err = err;
+            xbo[1].er = ent_r;
+            xbo[1].ew = ent_w;
             if (MZ_STAMPS) {
                 xl[2] = (long long)(__builtin_amdgcn_s_memtime() - ts[1]);  // its path levels
                 xl[3] = (long long)(ts[2] - ts[0]);                          // arrival at barrier (1)
@@ -4464,7 +4508,7 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
         lds_barrier();  // (2): its global stores stay in flight
         if constexpr (SEL && !kTreeLevels<NC>) {
             const int ncl = uni(xi[15]);
-            int e = uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]) | uni(xi[14]);
+            int e = bk_err<NC>(smem) | uni(xi[14]);
             tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, gdel, PS, D);
             if (w1g && pool && !e) {
                 // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[parent's hsx][t], after
@@ -4477,16 +4521,20 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
                     char *gdst = gather_out + (long long)t * row_bytes;
                     const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool |
                                       (long long)(uintptr_t)gather_out) & 15) == 0;
-                    if (al) {
-                        for (long long o0 = (long long)l * 16; o0 < row_bytes; o0 += 4 * 16 * kWave) {
-                            int4 v4[4];
-#pragma unroll
-                            for (int k = 0; k < 4; ++k)
-                                if (o0 + 16 * kWave * k < row_bytes) v4[k] = *(const int4 *)(src + o0 + 16 * kWave * k);
-#pragma unroll
-                            for (int k = 0; k < 4; ++k)
-                                if (o0 + 16 * kWave * k < row_bytes) *(int4 *)(gdst + o0 + 16 * kWave * k) = v4[k];
-                        }
+                    const long long o = (long long)l * 16, last = row_bytes - 16;
+                    if (al && row_bytes >= 16 && row_bytes <= 4 * 16 * kWave) {
+                        // up to 4 KiB: four 16-byte loads per lane issued together (offsets clamped
+                        // into the row, so no load is conditional), then the stores
+                        const int4 v0 = *(const int4 *)(src + (o < last ? o : last));
+                        const int4 v1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
+                        const int4 v2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
+                        const int4 v3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
+                        if (o < row_bytes) *(int4 *)(gdst + o) = v0;
+                        if (o + 1024 < row_bytes) *(int4 *)(gdst + o + 1024) = v1;
+                        if (o + 2048 < row_bytes) *(int4 *)(gdst + o + 2048) = v2;
+                        if (o + 3072 < row_bytes) *(int4 *)(gdst + o + 3072) = v3;
+                    } else if (al) {
+                        for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(gdst + o2) = *(const int4 *)(src + o2);
                     } else {
                         for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
                             *(int *)(gdst + o2) = *(const int *)(src + o2);
@@ -4695,11 +4743,16 @@ __global__ __launch_bounds__(kTreeWaves * 64) void k_tree(char *base, const floa
 #endif
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
-    err |= uni(xi[8]) | uni(xi[11]) | uni(xi[12]) | uni(xi[36]);  // the back-propagation waves
-    const float mmn = fminf(fminf(unif(xf[0]), unif(xf[2])), fminf(unif(xf[4]), unif(xf[6])));
-    const float mmx = fmaxf(fmaxf(unif(xf[1]), unif(xf[3])), fmaxf(unif(xf[5]), unif(xf[7])));
-    const int mm_cnt = (D >= 1 ? D : 0) + uni(xi[9]) + uni(xi[10]) + uni(xi[37]);  // path nodes 1..D: visited now
-    const long long ent_r = xl[0] + xl[11] + xl[13] + xl[19], ent_w = xl[1] + xl[12] + xl[14] + xl[20];
+    err |= bk_err<NC>(smem);  // the back-propagation waves
+    float mmn, mmx;
+    int mm_cnt;
+    bk_minmax<NC>(smem, D, mmn, mmx, mm_cnt);
+    long long ent_r = 0, ent_w = 0;
+#pragma unroll
+    for (int j = 1; j <= BK; ++j) {
+        ent_r += xbo[j].er;
+        ent_w += xbo[j].ew;
+    }
     const int ntot = err ? tot : tot + ncl;
     unsigned long long tp[4] = {0};
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
@@ -5318,7 +5371,7 @@ template <int NC, bool SEL = true>
 void launch_tree(mz_batch *b, const StepArgs &a) {
     const Geo &g = b->geo;
     const int flags = (b->fast_ok ? 1 : 0) | (g.B <= device_cus() ? 2 : 0);
-    hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(kTreeWaves * kWave), TreeLayout<NC>::total, b->stream,
+    hipLaunchKernelGGL((k_tree<NC, SEL>), dim3(g.B), dim3(kTreeWavesN<NC> * kWave), TreeLayout<NC>::total, b->stream,
                        (char *)b->dev.base, a.policy, a.beta, g.P, g.PS, g.B | (g.A << 24), a.pe | (g.K << 17), a.hsx,
                        a.K, a.discount, flags, a.reward, a.value, a.pool, a.pool_stride, a.row_bytes,
                        a.gather_out, a.idx_x, a.idy, a.act);
