@@ -4640,10 +4640,10 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     // and score from here on, while this wave expands
     lds_barrier();
     stamp(ts, 2);
-#ifndef MZ_SPANS_EPI
+#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP)
     const unsigned long long rm1 = span_mark();
 #else
-    unsigned long long rm1 = 0;
+    unsigned long long rm1 = 0, rm2 = 0, rm3 = 0;  // (diagnostic marks placed below)
 #endif
     const float r_in = unif(xf[60]), v_in = unif(xf[61]);  // (wave 1 staged them)
     // the sampling distribution and the K draws (std::discrete_distribution, two engine words per
@@ -4661,6 +4661,10 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             asm volatile("" ::"v"(cp));
             stamp(tq, 1);
         }
+#ifdef MZ_SPANS_EXP
+        asm volatile("" ::"v"(cp));
+        rm1 = span_mark();
+#endif
         if (!have_w) wait_vm();  // the words come from the window
         double u = 0.0;
         if (l < K) {
@@ -4683,6 +4687,10 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         asm volatile("" ::"v"(cnt));
         stamp(tq, 2);
     }
+#ifdef MZ_SPANS_EXP
+    asm volatile("" ::"v"(cnt));
+    rm2 = span_mark();
+#endif
     const long long st_old = (l < kStatN) ? sSt[l] : 0ll;
     // the leaf's children (cnode.cpp:264-293), in ascending action order
     wait_vm();  // the window landed: later waits need not drain this wave's stores
@@ -4726,6 +4734,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             d.Bn()[nb + leaf] = nbv;
         }
     }
+#ifdef MZ_SPANS_EXP
+    rm3 = span_mark();
+#endif
     if (l == 0) {
         xi[15] = ncl;
         xi[14] = err;
@@ -4736,10 +4747,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     stamp(ts, 3);
     lds_barrier();  // (2) back-propagation, prior scores, min/max partials and the children are in LDS
     stamp(ts, 4);
-#ifndef MZ_SPANS_EPI
+#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP)
     const unsigned long long rm2 = span_mark();
-#else
-    unsigned long long rm2 = 0;
 #endif
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
@@ -4886,10 +4895,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     }
     }
     stamp(ts, 6);
-#ifndef MZ_SPANS_EPI
+#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP)
     const unsigned long long rm3 = span_mark();
-#else
-    unsigned long long rm3 = 0;
 #endif
     if (SEL && l == 0) {
         idx_x[t] = err ? 0 : out_idx;
