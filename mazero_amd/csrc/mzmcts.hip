@@ -3966,26 +3966,51 @@ __device__ __forceinline__ void chase_next(int &v, int &cursor, int &x, int &Dn,
 
 // the back-propagation waves' exchange records (after barrier (2)): joined error word, min/max and
 // visited-node count (path nodes 1 .. D are visited now, cnode.cpp:431-447)
+// Lane j (1 <= j <= BK <= 7) reads record j, and three DPP steps within each row's first eight lanes
+// join them: min / max are exact and order-free (NaN partials lose to numbers, as in fminf), the
+// counts and error bits are integers.
+template <int NC>
+__device__ __forceinline__ void bk_join(const unsigned char *smem, int D, int &err, float &mn, float &mx, int &cnt) {
+    const BkOut *xb = (const BkOut *)(smem + TreeLayout<NC>::oXB);
+    const int j = lane_id() & 7;
+    const bool on = j >= 1 && j <= kBkN<NC>;
+    const int jj = on ? j : 1;
+    float a = xb[jj].mn, b = xb[jj].mx;
+    int c = xb[jj].cv, e = xb[jj].err;
+    if (!on) {
+        a = INFINITY;
+        b = -INFINITY;
+        c = 0;
+        e = 0;
+    }
+    a = fminf(a, i2f(dpp<0xB1>(f2i(a))));
+    b = fmaxf(b, i2f(dpp<0xB1>(f2i(b))));
+    c += dpp<0xB1>(c);
+    e |= dpp<0xB1>(e);
+    a = fminf(a, i2f(dpp<0x4E>(f2i(a))));
+    b = fmaxf(b, i2f(dpp<0x4E>(f2i(b))));
+    c += dpp<0x4E>(c);
+    e |= dpp<0x4E>(e);
+    a = fminf(a, i2f(dpp<0x141>(f2i(a))));
+    b = fmaxf(b, i2f(dpp<0x141>(f2i(b))));
+    c += dpp<0x141>(c);
+    e |= dpp<0x141>(e);
+    mn = unif(a);
+    mx = unif(b);
+    cnt = (D >= 1 ? D : 0) + uni(c);  // path nodes 1 .. D are visited now; record 1 counts 0
+    err = uni(e);
+}
 template <int NC>
 __device__ __forceinline__ int bk_err(const unsigned char *smem) {
-    const BkOut *xb = (const BkOut *)(smem + TreeLayout<NC>::oXB);
-    int e = 0;
-#pragma unroll
-    for (int j = 1; j <= kBkN<NC>; ++j) e |= uni(xb[j].err);
+    int e, c;
+    float a, b;
+    bk_join<NC>(smem, 0, e, a, b, c);
     return e;
 }
 template <int NC>
 __device__ __forceinline__ void bk_minmax(const unsigned char *smem, int D, float &mn, float &mx, int &cnt) {
-    const BkOut *xb = (const BkOut *)(smem + TreeLayout<NC>::oXB);
-    mn = unif(xb[1].mn);
-    mx = unif(xb[1].mx);
-    cnt = D >= 1 ? D : 0;
-#pragma unroll
-    for (int j = 2; j <= kBkN<NC>; ++j) {
-        mn = fminf(mn, unif(xb[j].mn));
-        mx = fmaxf(mx, unif(xb[j].mx));
-        cnt += uni(xb[j].cv);
-    }
+    int e;
+    bk_join<NC>(smem, D, e, mn, mx, cnt);
 }
 
 template <int NC>
