@@ -3590,13 +3590,17 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
 // staged record and run before the first.
 // --------------------------------------------------------------------------------------------
 // back-propagation waves of k_tree (waves 1 .. kBkN; wave 0 expands): seven (eight waves, two per
-// SIMD) for pools up to 384 nodes, whose trees hold one workgroup per CU; four (five waves) for the
-// larger classes, whose LDS then still fits two workgroups per CU (3s5z: 512 trees)
+// SIMD) for pools up to 384 nodes, whose trees hold one workgroup per CU, and for the 1,024-node
+// class, whose LDS (150 KB with seven) holds one workgroup per CU either way; four (five waves) for
+// the 512-node class, whose LDS then still fits two workgroups per CU (3s5z: 512 trees)
 #ifndef MZ_TREE_BK
 #define MZ_TREE_BK 7
 #endif
+#ifndef MZ_TREE_BK1024
+#define MZ_TREE_BK1024 MZ_TREE_BK
+#endif
 template <int NC>
-constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : 4;
+constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : (NC >= 1024 ? MZ_TREE_BK1024 : 4);
 template <int NC>
 constexpr int kTreeWavesN = kBkN<NC> + 1;
 constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
