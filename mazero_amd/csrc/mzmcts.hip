@@ -3599,11 +3599,18 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
 #ifndef MZ_TREE_BK1024
 #define MZ_TREE_BK1024 MZ_TREE_BK
 #endif
+#ifndef MZ_TREE_BK512
+#define MZ_TREE_BK512 MZ_TREE_BK
+#endif
 template <int NC>
-constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : (NC >= 1024 ? MZ_TREE_BK1024 : 4);
+constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : (NC >= 1024 ? MZ_TREE_BK1024 : MZ_TREE_BK512);
 template <int NC>
 constexpr int kTreeWavesN = kBkN<NC> + 1;
 constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
+// the 512-node class with seven back-propagation waves keeps two workgroups per CU (76 KB of LDS
+// each) with slots of 128 entries (S + 1 <= 128; larger searches take k_step)
+template <int NC>
+constexpr int kBkCapN = (NC == 512 && kBkN<NC> > 4) ? 128 : kBkCap;
 // per back-propagation wave, exchanged at barrier (2): its min/max partial, visited-node count,
 // error word and value-entry counters
 struct BkOut {
@@ -3616,7 +3623,7 @@ template <int NC>
 struct TreeLayout {
     static constexpr int r16(int x) { return (x + 15) & ~15; }
     static constexpr int BK = kBkN<NC>;
-    static constexpr int kTreeReg = (2 * BK * kBkCap > kRegCap) ? 2 * BK * kBkCap : kRegCap;  // staging int2s
+    static constexpr int kTreeReg = (2 * BK * kBkCapN<NC> > kRegCap) ? 2 * BK * kBkCapN<NC> : kRegCap;  // staging int2s
     static constexpr int PSx = NC / 2 + 1;                         // PS = S + 2 <= P / K <= NC / 2
     static constexpr int oA = 0;                                   // int4 [NC] staged {visit, prior, value, reward}
     static constexpr int oB = oA + r16(16 * NC);                   // int4 [NC] staged structure records
@@ -3713,7 +3720,7 @@ __device__ __forceinline__ void bk_path_records(const Dev &d, int t, int PS, int
 }
 
 // their value entries -> the wave's two staging slots (every entry of the node)
-template <int BK>
+template <int BK, int CAP>
 __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, int D, int k, int2 p0, int2 p1,
                                              int2 *sReg) {
     const int l = lane_id();
@@ -3724,9 +3731,9 @@ __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, 
         const int i = k + BK * j;
         const int2 pe = j == 0 ? p0 : p1;
         if (i > D) break;
-        if (pe.x < 0 || pe.x >= P || pe.y < 0 || pe.y > kBkCap) continue;  // (staged after barrier (1))
+        if (pe.x < 0 || pe.x >= P || pe.y < 0 || pe.y > CAP) continue;  // (staged after barrier (1))
         const int *src = (const int *)(gV + (size_t)pe.x * E);
-        int *dst = (int *)(sReg + (2 * k + j) * kBkCap);
+        int *dst = (int *)(sReg + (2 * k + j) * CAP);
         for (int c = 0; c < 2 * pe.y; c += kWave)
             if (c + l < 2 * pe.y) glds4a(src + c + l, dst + c);
         r.ndma += (2 * pe.y + kWave - 1) / kWave;
@@ -3764,7 +3771,7 @@ __device__ __forceinline__ void bk_boot(const Lds &s, float *boot, int D, float 
 }
 
 // wave k's path levels k, k + BK, ... (CTree::back_propagate, cnode.cpp:415-450, node by node)
-template <int BK>
+template <int BK, int CAP>
 __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds &s, const float4 *sCn, float2 *sAz,
                                           const float *boot, int2 *sReg, BkPre pre, int t, int D, float reward,
                                           float disc, int k, int &err, long long &ent_r, long long &ent_w, float &pmn,
@@ -3789,7 +3796,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             n = uni(pe.x);
             nv = uni(pe.y);
         }
-        if (n < 0 || n >= g.P || nv < 0 || nv > kBkCap) {
+        if (n < 0 || n >= g.P || nv < 0 || nv > CAP) {
             err |= kErrPath;
             continue;
         }
@@ -3803,11 +3810,11 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         const float key = boot[i];
         const int2 *R;
         if (j == 0 && pre.nv0 >= 0) {
-            R = sReg + (2 * k) * kBkCap;
+            R = sReg + (2 * k) * CAP;
         } else if (j == 1 && pre.nv1 >= 0) {
-            R = sReg + (2 * k + 1) * kBkCap;
+            R = sReg + (2 * k + 1) * CAP;
         } else {  // a later level (or a pre-stage that did not match): slot 0, free once level j - 2 is done
-            int2 *dst = sReg + (2 * k) * kBkCap;
+            int2 *dst = sReg + (2 * k) * CAP;
             const int *src = (const int *)(gV + (size_t)n * g.E);
             for (int c = 0; c < 2 * nv; c += kWave)
                 if (c + l < 2 * nv) glds4a(src + c + l, (int *)dst + c);
@@ -4372,7 +4379,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                     }
                 }
         // this wave's path levels' value entries: issued last, in flight across barrier (1)
-        const BkPre pre = bk_prestage<BK>(d, t, P, g.E, D, wv - 1, bp0, bp1, (int2 *)(smem + L::oReg));
+        const BkPre pre = bk_prestage<BK, kBkCapN<NC>>(d, t, P, g.E, D, wv - 1, bp0, bp1, (int2 *)(smem + L::oReg));
         wait_vm_but(pre.ndma);
         stamp(ts, 1);
         lds_barrier();  // (1)
@@ -4390,7 +4397,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         int berr = 0;
         long long ber = 0, bew = 0;
         float bmn, bmx;
-        bk_levels<BK>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+        bk_levels<BK, kBkCapN<NC>>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, wv - 1, berr, ber, bew, bmn, bmx);
         stamp(ts, 3);
         // nodes 1 .. tot-1 in 64-node blocks dealt round-robin over waves 2 .. kBk, the deepest
@@ -4495,7 +4502,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             return;
         }
         stamp(tw1, 1);
-        const BkPre pre = bk_prestage<BK>(d, t, P, g.E, D, 0, bp0, bp1, (int2 *)(smem + L::oReg));
+        const BkPre pre = bk_prestage<BK, kBkCapN<NC>>(d, t, P, g.E, D, 0, bp0, bp1, (int2 *)(smem + L::oReg));
         stamp(tw1, 2);
         wait_vm_but(pre.ndma);  // the lambda powers, reward and value (the entries stay in flight)
         stamp(tw1, 3);
@@ -4516,7 +4523,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         int err = 0;
         long long ent_r = 0, ent_w = 0;
         float pmn, pmx;
-        bk_levels<BK>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+        bk_levels<BK, kBkCapN<NC>>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, 0, err, ent_r, ent_w, pmn, pmx, tl);
         if (l == 0) {
             xbo[1].mn = pmn;
@@ -5719,7 +5726,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         if (chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave > 160 * 1024) b->chain_nc = -1;
     }
     // (k_tree stages one path node's value entries per slot: E <= kBkCap)
-    if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= kBkCap && !getenv_flag("MZ_NO_TREE")) b->tree_nc = b->nc;
+    if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE"))
+        b->tree_nc = b->nc;
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
