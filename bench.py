@@ -338,7 +338,7 @@ def fused_kernel_name(K: int, P: int) -> str:
     if K == 1:
         return "k_chain (K = 1 chains: fused expand+backup+select+gather)"
     if 2 <= K <= 64 and P <= 1024:
-        return "k_tree (eight waves up to 384 nodes, five above: fused expand+backup+select+gather)"
+        return "k_tree (eight waves: fused expand+backup+select+gather)"
     return "k_step<true,true> (fused expand+backup+select+gather)"
 
 
