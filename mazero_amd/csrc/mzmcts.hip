@@ -3916,6 +3916,18 @@ constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 template <int NC>
 constexpr bool kTreeLevels = (NC >= 1024);
 
+// pb_c of the prior scores from the host table in HBM (one gather per node, L2-resident) instead of
+// the staged per-n factors and a double division per node: the gather's wait leaves the SIMD to the
+// wave that shares it.  Same-box A/B: 3s5z K = 5 10.50 -> 10.38 us, 3m K = 5 unchanged;
+// MZ_PBC_FACTORS builds the factor path for A/B runs
+#ifdef MZ_PBC_FACTORS
+template <int NC>
+constexpr bool kTreePbTable = kTreeLevels<NC>;
+#else
+template <int NC>
+constexpr bool kTreePbTable = true;
+#endif
+
 // Who stages the value-set scalars in round 1: wave 0 (with the path, the flags and the leaf's
 // inputs) or, for the 1024-node class, wave 4.  Same-box A/B: 3m K = 10 9.77 -> 9.64 us with wave 4;
 // the smaller classes measured no gain (3m K = 5) or a loss (3s5z K = 5, 10.47 -> 10.59 us).
@@ -4348,7 +4360,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             for (int k = 0; k < MZ_ABL_LINES; ++k) glds16a((const char *)gVt + 1024 * k + 16 * l, smem + L::oReg + 1024 * k);
         }
 #endif
-        if (SEL && !kTreeLevels<NC> && wv == 3) {  // the pUCT factors per parent visit count (no gathers)
+        if (SEL && !kTreePbTable<NC> && wv == 3) {  // the pUCT factors per parent visit count (no gathers)
             dma_dwords(d.pb(), lds_addr(smem) + L::oPb, PS, true);
             dma_dwords(d.sq(), lds_addr(smem) + L::oSq, 2 * PS, true);
         }
@@ -4425,7 +4437,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                     // pb_c (cnode.cpp:313-314): the host-built table for the 1024-node class (its many
                     // nodes make the double division cost more than the gathers), else from the
                     // staged per-n factors with the same double arithmetic
-                    if constexpr (kTreeLevels<NC>) pbc[k] = T[np * (np + 1) / 2 + v];
+                    if constexpr (kTreePbTable<NC>) pbc[k] = T[np * (np + 1) / 2 + v];
                     else pbc[k] = (float)((double)spb[np] * (ssq[np] / (double)(v + 1)));
                 }
                 if (a.x > 0 && !fn) {
