@@ -147,6 +147,13 @@ BIG = [
     ("deep_k2", 64, 9, 2, 200, 0.0),
     # value sets longer than a k_tree staging slot (E = 401 > kBkCap): the handle falls back to k_step
     ("k2_long_value_sets", 32, 9, 2, 400, 0.0),
+    # deep K = 2 paths inside the 256-node class (seven back-propagation waves): levels past a
+    # wave's two pre-staged ones (i + 14, ...) are staged after the first barrier
+    ("deep_k2_tree", 64, 9, 2, 120, 0.0),
+    # the 512-node class keeps 128-entry staging slots (two workgroups per CU): E = 151 takes k_step,
+    # E = 101 k_tree
+    ("k3_512_class_kstep", 64, 9, 3, 150, 0.0),
+    ("k4_512_class_tree", 64, 9, 4, 100, 0.0),
 ]
 
 
