@@ -4475,6 +4475,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 xl[wv + 6] = (long long)(__builtin_amdgcn_s_memtime() - ts[2]);  // (xl[8], xl[9]) all work after (1)
             }
         }
+#ifdef MZ_SPANS_B2
+        if (l == 0) xl[1 + wv] = (long long)span_mark();  // (diagnostic: arrival at barrier (2))
+#endif
         lds_barrier();  // (2)
         if (SEL && !kTreeLevels<NC> && wv < 4) {
             const int ncl = uni(xi[15]), err = bk_err<NC>(smem) | uni(xi[14]);
@@ -4553,6 +4556,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 xl[18] = (long long)(tw1[3] - tw1[1]);                       // round 1: pre-stage, path landed
             }
         }
+#ifdef MZ_SPANS_B2
+        if (l == 0) xl[2] = (long long)span_mark();  // (diagnostic: arrival at barrier (2))
+#endif
         lds_barrier();  // (2): its global stores stay in flight
         if constexpr (SEL && !kTreeLevels<NC>) {
             const int ncl = uni(xi[15]);
@@ -4688,7 +4694,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     // and score from here on, while this wave expands
     lds_barrier();
     stamp(ts, 2);
-#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP)
+#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP) && !defined(MZ_SPANS_B2)
     const unsigned long long rm1 = span_mark();
 #else
     unsigned long long rm1 = 0, rm2 = 0, rm3 = 0;  // (diagnostic marks placed below)
@@ -4793,10 +4799,20 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         xi[62] = wbase;
     }
     stamp(ts, 3);
+#ifdef MZ_SPANS_B2
+    const unsigned long long b2own = span_mark();
+#endif
     lds_barrier();  // (2) back-propagation, prior scores, min/max partials and the children are in LDS
     stamp(ts, 4);
-#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP)
+#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP) && !defined(MZ_SPANS_B2)
     const unsigned long long rm2 = span_mark();
+#endif
+#ifdef MZ_SPANS_B2  // wave 0's own arrival, the last of roles 1-3, the last of roles 4-7
+    rm1 = b2own;
+    rm2 = (unsigned long long)xl[2];
+    rm3 = (unsigned long long)xl[5];
+    for (int j = 3; j <= 4; ++j) rm2 = (unsigned long long)xl[j] > rm2 ? (unsigned long long)xl[j] : rm2;
+    for (int j = 6; j <= BK + 1; ++j) rm3 = (unsigned long long)xl[j] > rm3 ? (unsigned long long)xl[j] : rm3;
 #endif
 
     // ---- the selection of the next simulation (cnode.cpp:381-413) ----
@@ -4943,7 +4959,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     }
     }
     stamp(ts, 6);
-#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP)
+#if !defined(MZ_SPANS_EPI) && !defined(MZ_SPANS_EXP) && !defined(MZ_SPANS_B2)
     const unsigned long long rm3 = span_mark();
 #endif
     if (SEL && l == 0) {
