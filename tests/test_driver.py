@@ -493,3 +493,105 @@ def test_captured_memset_node_keeps_loop_eager(port_lib):
             assert memsets == S and lp.graph is False
         else:
             assert memsets == 0 and isinstance(lp.graph, torch.cuda.CUDAGraph)
+
+
+# ------------------------------------------------------------------------------------------------
+# Reference-driver fixtures (oracle/gen_driver_golden.py: core/mcts/tree_search/mcts_sampled.py
+# itself, imported in the build container, over the reference ctree)
+# ------------------------------------------------------------------------------------------------
+from driver_fixture import DriverFixture, ReplayNet, driver_fixtures  # noqa: E402
+
+_DRIVER_FX = driver_fixtures()
+_fx_id = lambda p: os.path.basename(p)[7:-4]  # noqa: E731
+
+
+def test_driver_fixtures_present():
+    assert len(_DRIVER_FX) >= 6, "tests/golden/driver_*.npz missing (python oracle/gen_driver_golden.py)"
+
+
+def _u32(a):
+    a = np.asarray(a)
+    return a.view(np.uint32) if a.dtype == np.float32 else a
+
+
+@pytest.mark.parametrize("path", _DRIVER_FX, ids=_fx_id)
+def test_root_inputs_match_reference_driver(path):
+    """The product's host-side root preprocessing (SampledMCTS.root_inputs) against the arguments
+    the reference driver passed to prepare (mcts_sampled.py:64-106) and the tree seed it drew
+    (:89), bit for bit, and the generator consumed identically."""
+    import torch
+
+    from mazero_amd.mcts_sampled import SampledMCTS
+
+    fx = DriverFixture(path)
+    z = fx.z
+    rng = fx.np_random()
+    (rr, rv, rp, rb, eps, rn), seed = SampledMCTS(fx.config(), rng).root_inputs(
+        fx.root_output(torch.device("cpu")), fx.agent, fx.legal, fx.meta["add_noise"], 1.0)
+    assert seed == fx.meta["tree"]["seed"]
+    assert eps == float(z["prep_eps"])
+    for got, key in ((rr, "prep_rewards"), (rv, "prep_values"), (rp, "prep_probs"), (rb, "prep_beta"),
+                     (rn, "prep_noises")):
+        exp = z[key]
+        assert got.dtype == exp.dtype and got.shape == exp.shape, key
+        np.testing.assert_array_equal(_u32(got), _u32(exp), err_msg=key)
+
+
+@pytest.mark.parametrize("tree", ["port", "ref"])
+@pytest.mark.parametrize("path", _DRIVER_FX, ids=_fx_id)
+def test_oracle_driver_matches_reference_driver(path, tree, request):
+    """oracle/driver.py (the restatement every GPU driver test checks against) reproduces the
+    reference driver's run: the tree calls of every simulation, the network's inputs, the
+    SearchOutput and the generator state afterwards."""
+    import types
+
+    import torch
+
+    from driver import OracleSampledMCTS
+
+    lib = request.getfixturevalue("port_lib" if tree == "port" else "ref_lib")
+    fx = DriverFixture(path)
+    z = fx.z
+    cpu = torch.device("cpu")
+    net = ReplayNet(fx, cpu)
+    rng = fx.np_random()
+    drv = OracleSampledMCTS(fx.config(), rng, lib, record=True)
+    res = drv.batch_search(net, fx.root_output(cpu), fx.agent, fx.factor, fx.N, fx.legal, device=cpu,
+                           add_noise=fx.meta["add_noise"])
+    net.check_inputs()
+    for s, t in enumerate(drv.trace):
+        np.testing.assert_array_equal(t["idx"], z["sel_idx"][s], err_msg=f"idx_x sim {s}")
+        np.testing.assert_array_equal(t["act"], z["sel_act"][s].reshape(-1), err_msg=f"action sim {s}")
+        for k in ("reward", "value", "probs", "beta"):
+            np.testing.assert_array_equal(_u32(t[k]).reshape(-1), _u32(z["exp_" + k][s]).reshape(-1),
+                                          err_msg=f"{k} sim {s}")
+    _compare_outputs(types.SimpleNamespace(**res), fx.expected())
+    np.testing.assert_array_equal(np.asarray(rng.random(4)), z["rng_after"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", _DRIVER_FX, ids=_fx_id)
+def test_device_driver_matches_reference_driver(path):
+    """mazero_amd.mcts_sampled.SampledMCTS, fed the reference network's recorded outputs,
+    reproduces the reference driver's search bit for bit: the leaf rows it gathers and the joint
+    actions it builds (the network's inputs), every SearchOutput field and the np_random state
+    after the search -- eagerly, then captured into a HIP graph and replayed, then replayed again."""
+    import torch
+
+    from mazero_amd.mcts_sampled import _LOOPS, SampledMCTS
+
+    fx = DriverFixture(path)
+    dev = torch.device("cuda", 0)
+    net = ReplayNet(fx, dev)
+    root = fx.root_output(dev)
+    for run in range(3):  # eager, capture + replay, replay
+        net.reset()
+        rng = fx.np_random()
+        got = SampledMCTS(fx.config(), rng).batch_search(net, root, fx.agent, fx.factor, fx.N, fx.legal, device=dev,
+                                                         add_noise=fx.meta["add_noise"])
+        torch.cuda.synchronize()
+        net.check_inputs()
+        _compare_outputs(got, fx.expected())
+        np.testing.assert_array_equal(np.asarray(rng.random(4)), fx.z["rng_after"])
+    loop = [v for v in _LOOPS.values() if v.model_ref() is net][0]
+    assert isinstance(loop.graph, torch.cuda.CUDAGraph), "the third search did not replay a graph"
