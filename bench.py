@@ -10,7 +10,7 @@ Per search the device executes exactly what mazero_amd.mcts_sampled runs around 
   49 x fused <expand+backup, select, gather>  ->  1 x <expand+backup>  ->  one k_readback
 where the fused kernel is k_chain3 (K = 1, pools <= 256 nodes), k_chain (K = 1, larger pools), k_tree
 (2 <= K <= 64, pools <= 1024 nodes) or k_step
-(fused_kernel_name below)
+(as the library reports it, mz_fused_kernel)
 with the network replaced by synthetic device-resident outputs (softmax(N(0,1))
 policy = beta, reward 0.1*N(0,1), value N(0,1), Dirichlet(0.3) root noise, hidden-state pool
 [51, 256, 3*128] fp32 that the fused kernel gathers from).  The whole step (3 searches) is
@@ -264,7 +264,7 @@ class HipLeg:
         achieved = bytes_per_launch / avg / 1e9
         pmc = pmc_traffic(self.args)
         r = dict(
-            kernel=fused_kernel_name(K, K * (S + 2)),
+            kernel=fused_kernel_name(tb0),
             bound="hbm",
             achieved=round(achieved, 3),
             peak=8000.0,
@@ -330,16 +330,16 @@ def launch_spans(spans, S, B):
                 period_us=round(float(t1[-1] - t0[0]) / 1e3 / len(body), 3), wave_us=wave)
 
 
-def fused_kernel_name(K: int, P: int) -> str:
-    """The per-simulation fused kernel the library launches for sampled_times K and a pool of P
-    nodes (launch_step in mazero_amd/csrc/mzmcts.hip)."""
-    if K == 1 and P <= 256:
-        return "k_chain3 (K = 1 chains, three waves: fused expand+backup+select+gather)"
-    if K == 1:
-        return "k_chain (K = 1 chains: fused expand+backup+select+gather)"
-    if 2 <= K <= 64 and P <= 1024:
-        return "k_tree (eight waves: fused expand+backup+select+gather)"
-    return "k_step<true,true> (fused expand+backup+select+gather)"
+def fused_kernel_name(tb) -> str:
+    """The per-simulation fused kernel the library launches for this handle, as the library itself
+    reports it (mz_fused_kernel: chosen at mz_create from the geometry and MZ_CHAIN_V2 /
+    MZ_NO_CHAIN / MZ_NO_TREE)."""
+    if not hasattr(tb._lib, "mz_fused_kernel"):  # (an older experiment build, MZ_LIB_OVERRIDE)
+        return "unknown (library without mz_fused_kernel)"
+    k = tb.fused_kernel()
+    what = {"k_chain3": "K = 1 chains, three waves", "k_chain": "K = 1 chains, two waves",
+            "k_tree": "eight waves", "k_step": "general kernel"}[k.split("<")[0]]
+    return f"{k} ({what}: fused expand+backup+select+gather)"
 
 
 class DropinLeg:
@@ -699,6 +699,39 @@ def physical_cores():
         return None
 
 
+def cpu_quota():
+    """This process's CPU bandwidth limit from its cgroup (v2 cpu.max, else v1 cfs quota/period):
+    {"cpus": quota / period or None when unlimited, "source": file, "raw": its content}, or None."""
+    cands = ["/sys/fs/cgroup/cpu.max"]
+    try:  # the process's own cgroup path (v2 "0::/path", v1 "...:cpu,cpuacct:/path")
+        with open("/proc/self/cgroup") as f:
+            for line in f:
+                parts = line.strip().split(":", 2)
+                if len(parts) == 3 and parts[0] == "0":
+                    cands.insert(0, "/sys/fs/cgroup" + parts[2].rstrip("/") + "/cpu.max")
+                elif len(parts) == 3 and "cpu" in parts[1].split(","):
+                    cands.append(("/sys/fs/cgroup/cpu,cpuacct" + parts[2].rstrip("/"), "v1"))
+    except OSError:
+        pass
+    cands += [("/sys/fs/cgroup/cpu,cpuacct", "v1"), ("/sys/fs/cgroup/cpu", "v1")]
+    for c in cands:
+        try:
+            if isinstance(c, tuple):
+                with open(c[0] + "/cpu.cfs_quota_us") as f:
+                    q = int(f.read().strip())
+                with open(c[0] + "/cpu.cfs_period_us") as f:
+                    per = int(f.read().strip())
+                return {"cpus": round(q / per, 3) if q > 0 else None, "source": c[0] + "/cpu.cfs_{quota,period}_us",
+                        "raw": f"{q} {per}"}
+            with open(c) as f:
+                raw = f.read().strip()
+            q, per = raw.split()[:2]
+            return {"cpus": None if q == "max" else round(int(q) / int(per), 3), "source": c, "raw": raw}
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
     """The reference CPU ctree (or the CPU port), one host core, tree calls only, same inputs; plus
     SURVEY §8(d)(ii): the same env steps on several host cores at once, one process per core with
@@ -745,7 +778,11 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
         share = sorted(os.sched_getaffinity(0))
     except AttributeError:
         share = list(range(os.cpu_count() or 1))
-    n_proc = max(1, min(procs, len(share), B))
+    # the CPU time this job may use: the affinity mask lists every CPU of the host on a GPU box, the
+    # cgroup's bandwidth quota is what bounds it (one GPU's share of the node)
+    quota = cpu_quota()
+    q_cpus = int(quota["cpus"]) if quota and quota["cpus"] else None
+    n_proc = max(1, min(procs, len(share), B, q_cpus or procs))
     ctx = mp.get_context("spawn")  # a fresh interpreter per worker (this process may hold the GPU)
     start, q = ctx.Event(), ctx.Queue()
     workers = []
@@ -762,7 +799,7 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
         w.join(timeout=30)
     wall = max(r[2] for r in res)
     total = sum(r[0] for r in res)
-    multi = {"value": round(total / wall, 1), "processes": n_proc, "cores": n_proc,
+    multi = {"value": round(total / wall, 1), "processes": n_proc, "cores": n_proc, "cgroup_cpu_quota": quota,
              "sample": f"{total} sims in {wall:.1f} s wall: {n_proc} processes, each searching its shard of "
                        f"the {B} roots of every agent search ({kind} ctree)"}
     # the whole host: a GPU box grants this job one GPU's share of the node's CPUs (16), so every
@@ -772,8 +809,10 @@ def cpu_baseline(host_inputs, B, A, K, S, N, budget_s, procs=16, ptree=False):
         multi["whole_host_projection"] = {
             "value": round(total / wall / n_proc * phys, 1), "cores": phys,
             "basis": f"measured rate per process at {n_proc} processes x {phys} physical cores (linear: an upper "
-                     f"bound on the reference ctree's whole-host throughput); not measured, the pool allows "
-                     f"{n_proc} CPUs per one-GPU box"}
+                     f"bound on the reference ctree's whole-host throughput); not measured: this job's cgroup "
+                     f"grants {quota['cpus'] if quota else 'an unknown number of'} CPUs of bandwidth "
+                     f"({quota['source'] + ' = ' + quota['raw'] if quota else 'no cgroup limit file found'}), "
+                     f"while the affinity mask lists {len(share)}"}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:

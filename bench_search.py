@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--ref-steps", type=int, default=2)
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--device-only", action="store_true",
+                    help="only the graph-replayed device loop (profiling runs: with MZ_TRACE_MARKS=1 two one-element "
+                         "fills mark its timed region for scripts/search_split.py)")
     args = ap.parse_args()
 
     import torch
@@ -74,21 +77,34 @@ def main():
                               for a, v in zip(res.sampled_actions, res.sampled_visit_count)]
         return res
 
-    def timed(mcts, steps, warm):
+    def mark(k):  # (MZ_TRACE_MARKS=1: FillFunctor<short> in a rocprofv3 kernel trace, outside the timing)
+        if os.environ.get("MZ_TRACE_MARKS") == "1":
+            torch.full((1,), k, dtype=torch.int16, device=dev)
+
+    def timed(mcts, steps, warm, marks=False):
         for i in range(warm):
             env_step(mcts, i)
+        if marks:
+            mark(1)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
             env_step(mcts, i)
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) / steps
+        t = (time.perf_counter() - t0) / steps
+        if marks:
+            mark(2)
+        return t
 
     sims_per_step = B * S * N
     line = {"metric": f"full search loop simulations/s, SMAC {args.map} ({N} agents x {B} roots x {S} sims, K={K})",
             "unit": "simulations/s", "network": "MuZeroShapedNet (MLP heads, random init, autocast)"}
-    t = timed(SampledMCTS(cfg, np.random.RandomState(0), use_graph=True), args.steps, 2)
+    t = timed(SampledMCTS(cfg, np.random.RandomState(0), use_graph=True), args.steps, 2, marks=True)
     line["device"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3)}
+    if args.device_only:
+        line["steps"] = args.steps
+        print(json.dumps(line), flush=True)
+        return
     t = timed(SampledMCTS(cfg, np.random.RandomState(0), use_graph=False), max(1, args.steps // 2), 1)
     line["device_eager"] = {"value": round(sims_per_step / t, 1), "ms_per_step": round(t * 1e3, 3)}
 

@@ -60,13 +60,21 @@ int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_age
                     const int32_t *factor, int factor_cols, const int32_t *actions, int64_t *joint_out);
 
 /* Census of a captured, not yet instantiated HIP graph (`graph` is a hipGraph_t): its node count
- * and how many of them are runtime memset nodes.  Under the runtime's default graph packet capture
- * a replayed hipMemsetAsync node can write a stale fill pattern instead of its value once enough
+ * and how many of them are runtime memset nodes, child-graph nodes' graphs counted recursively.
+ * Under the runtime's default graph packet capture a replayed hipMemsetAsync node can write a
+ * stale fill pattern instead of its value once enough
  * eager work has run (scripts/memset_graph_repro.py); no mz_* call records one, but
  * the model's own ops inside a captured search loop might (the reference driver has no graph,
  * mcts_sampled.py:114-172).  mazero_amd.mcts_sampled runs such a loop eagerly instead of replaying
  * it. */
 int mz_graph_census(void *graph, int *total_nodes, int *memset_nodes);
+
+/* The kernel this handle launches for a fused simulation step (mz_expand_backup_select), as a
+ * NUL-terminated name written into out[len]: "k_chain3<NC>", "k_chain<NC>", "k_tree<NC>",
+ * "k_step<NC>" or "k_step<0,joint>" (NC = the compile-time node class, 0 = run-time layout).
+ * Chosen at mz_create from the geometry (and MZ_CHAIN_V2 / MZ_NO_CHAIN / MZ_NO_TREE); for the
+ * bench's roofline label and the tests that pin which path ran. */
+int mz_fused_kernel(mz_batch *b, char *out, int len);
 
 #ifdef __cplusplus
 }

@@ -111,6 +111,7 @@ DRIVER_SIGNATURES = {
     "mz_policy_glue": (_i, [_p, _p, _i, _i64, _i64, _f, _p, _p]),
     "mz_joint_action": (_i, [_p, _p, _i, _i, _i, _p, _i, _p, _p]),
     "mz_graph_census": (_i, [_p, C.POINTER(_i), C.POINTER(_i)]),
+    "mz_fused_kernel": (_i, [_p, C.c_char_p, _i]),
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 
@@ -154,8 +155,9 @@ def bind(lib: C.CDLL) -> C.CDLL:
         "mz_print": (_i, [_p]),
     }
     if hasattr(lib, "mz_policy_glue"):  # include/mzdriver.h: product library only
-        sig.update(DRIVER_SIGNATURES)
-        sig.update(CONSUME_SIGNATURES)
+        # (an experiment build of an older source, MZ_LIB_OVERRIDE, may lack newer entry points:
+        # bound when present; tests/test_capi.py checks that the product exports every one)
+        sig.update({k: v for k, v in {**DRIVER_SIGNATURES, **CONSUME_SIGNATURES}.items() if hasattr(lib, k)})
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res

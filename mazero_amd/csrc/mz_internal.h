@@ -12,6 +12,8 @@ extern "C" {
 MZ_HIDDEN int mz_internal_fail(int code, const char *msg);
 // Make the handle's device current and report its batch size, action count and stream.
 MZ_HIDDEN int mz_internal_launch_info(mz_batch *b, int *B, int *A, hipStream_t *stream);
+// after a launch on the handle's stream: record its order event (mz_set_stream)
+MZ_HIDDEN void mz_internal_enqueued(mz_batch *b);
 // agent_num of the handle (0 for a null handle).
 MZ_HIDDEN int mz_internal_agent_num(mz_batch *b);
 }  // extern "C"

@@ -178,6 +178,7 @@ int mz_select_actions(mz_batch *b, const int32_t *degrees, const int32_t *visits
     hipLaunchKernelGGL(k_select_actions, dim3((B + kLanes - 1) / kLanes), dim3(kLanes), 0, stream, B,
                        mz_internal_agent_num(b), (const int *)degrees, (const int *)visits, (const int *)actions,
                        width, ipow, e, deterministic, uniforms, (int *)pos_out, (int *)action_out, entropy_out);
+    mz_internal_enqueued(b);
     return launch_status();
 }
 
@@ -191,6 +192,7 @@ int mz_eps_greedy(mz_batch *b, const int32_t *legal, int64_t legal_stride, float
     if (legal_stride < A) return mz_internal_fail(MZ_ERR_ARG, "mz_eps_greedy: legal rows hold fewer than A entries");
     hipLaunchKernelGGL(k_eps_greedy, dim3((B + kLanes - 1) / kLanes), dim3(kLanes), 0, stream, B, A,
                        (const int *)legal, (long long)legal_stride, eps, u_eps, u_cat, (int *)action_io);
+    mz_internal_enqueued(b);
     return launch_status();
 }
 
@@ -209,6 +211,7 @@ int mz_marginal_policy(mz_batch *b, const int32_t *marginal, int64_t marginal_st
     hipLaunchKernelGGL(k_marginal_policy, dim3((B + kLanes - 1) / kLanes), dim3(kLanes), 0, stream, B, A,
                        (const int *)marginal, (long long)marginal_stride, (const int *)legal, (long long)legal_stride,
                        mode, (int *)action_io, prob_io, entropy_out);
+    mz_internal_enqueued(b);
     return launch_status();
 }
 

@@ -181,6 +181,7 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
     else
         hipLaunchKernelGGL(k_policy_glue<false>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
                            (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out);
+    mz_internal_enqueued(b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
     return MZ_OK;
@@ -208,29 +209,45 @@ int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_age
         hipLaunchKernelGGL(k_joint_action<false>, dim3(B), dim3(kWave), 0, stream, pred_logits, num_agents, A,
                            current_agent, (const int *)factor, factor_cols, (const int *)actions,
                            (long long *)joint_out);
+    mz_internal_enqueued(b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
     return MZ_OK;
 }
 
-int mz_graph_census(void *graph, int *total_nodes, int *memset_nodes) {
-    if (!graph || !total_nodes || !memset_nodes) return mz_internal_fail(MZ_ERR_ARG, "mz_graph_census: null argument");
-    hipGraph_t g = (hipGraph_t)graph;
+// nodes and memset nodes of a graph, child graphs (hipGraphNodeTypeGraph: a nested capture, an
+// embedded graph) included
+static hipError_t census(hipGraph_t g, int depth, int *total, int *memsets) {
+    if (depth > 16) return hipErrorInvalidValue;
     size_t n = 0;
     hipError_t e = hipGraphGetNodes(g, nullptr, &n);
-    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    if (e != hipSuccess) return e;
     hipGraphNode_t *nodes = (hipGraphNode_t *)malloc(sizeof(hipGraphNode_t) * (n ? n : 1));
-    if (!nodes) return mz_internal_fail(MZ_ERR_RUNTIME, "mz_graph_census: out of host memory");
+    if (!nodes) return hipErrorOutOfMemory;
     e = hipGraphGetNodes(g, nodes, &n);
-    int ms = 0;
+    *total += (int)n;
     for (size_t k = 0; e == hipSuccess && k < n; ++k) {
         hipGraphNodeType ty;
         e = hipGraphNodeGetType(nodes[k], &ty);
-        if (e == hipSuccess && ty == hipGraphNodeTypeMemset) ++ms;
+        if (e != hipSuccess) break;
+        if (ty == hipGraphNodeTypeMemset) {
+            ++*memsets;
+        } else if (ty == hipGraphNodeTypeGraph) {
+            hipGraph_t child = nullptr;
+            e = hipGraphChildGraphNodeGetGraph(nodes[k], &child);
+            if (e == hipSuccess) e = census(child, depth + 1, total, memsets);
+        }
     }
     free(nodes);
+    return e;
+}
+
+int mz_graph_census(void *graph, int *total_nodes, int *memset_nodes) {
+    if (!graph || !total_nodes || !memset_nodes) return mz_internal_fail(MZ_ERR_ARG, "mz_graph_census: null argument");
+    int total = 0, ms = 0;
+    hipError_t e = census((hipGraph_t)graph, 0, &total, &ms);
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
-    *total_nodes = (int)n;
+    *total_nodes = total;
     *memset_nodes = ms;
     return MZ_OK;
 }

@@ -10,7 +10,8 @@
 // back-propagation of simulation s with the selection of s+1 and the leaf hidden-state gather.
 //
 // Data layout in HBM (tree-major structure of arrays; node n of tree t at index t*P + n, where
-// P = K*(S+2) is the reference's per-root pool, cnode.cpp:562):
+// P = 1 + min(K, A^N)*(S+1) is the nodes a search can create; the reference allocates K*(S+2),
+// cnode.cpp:562):
 //   A[t][n]  int4  {visit, prior, value, reward}           (value = ws/tw, 0 while unexpanded)
 //   Bn[t][n] int4  {first_child, nc | action<<8 | (maxdepth+1)<<16, pred_value, hidden_state_index_x}
 //   Q[t][n]  float q = qsa - parent.pred_value, the node's member of the min/max set (cnode.cpp:435,445)
@@ -36,7 +37,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/mzmcts.h"
@@ -486,7 +489,7 @@ struct Lds {
     int *il;  // internal-node list of the precomputed walk (layout classes)
 };
 
-// LDS layout of k_step.  Capacity classes NC = 64 .. 1024 (node pool K*(S+2) <= NC) have a
+// LDS layout of k_step.  Capacity classes NC = 64 .. 1024 (node pool P <= NC) have a
 // compile-time layout: every LDS address folds into an instruction's immediate offset and no
 // offset occupies an SGPR for the kernel's lifetime.  NC = 0 is the general layout, whose offsets
 // come from Geo (trees above 1024 nodes).  The compile-time classes compute pUCT coefficients from
@@ -3037,9 +3040,12 @@ struct Chain3Args {  // k_chain3's parameter list, for the kernel-argument offse
     const float *policy, *beta, *reward, *value;
     int ppk, bak, hsx;
     float discount;
+    const char *src_slot;
     ChainIO io;
 };
-static_assert(offsetof(Chain3Args, io) == 56 && sizeof(ChainIO) == 56, "k_chain3 argument layout");
+// (the first 16 dwords, through src_slot, arrive preloaded in SGPRs)
+static_assert(offsetof(Chain3Args, src_slot) == 56 && offsetof(Chain3Args, io) == 64 && sizeof(ChainIO) == 56,
+              "k_chain3 argument layout");
 #ifdef __HIP_DEVICE_COMPILE__
 typedef const __attribute__((address_space(4))) ChainIO cChainIO;
 #else
@@ -3097,17 +3103,19 @@ struct Chain3Layout {
 };
 int chain3_lds_bytes(int nc) { return Chain3Layout<0>(nc).total; }
 
-// ROW: the leaf-row gather's class -- 0 any row (copied after the barrier), 1 16-byte aligned rows of
-// <= 4 KiB (registers), 2 aligned rows of <= 16 KiB (LDS-DMA), 3 no gather (no pool, or no selection)
+// ROW: the leaf-row gather's class -- 0 any row, 1 16-byte aligned rows of <= 4 KiB (registers), 2
+// aligned rows of <= 16 KiB (LDS-DMA), 3 no gather (no pool, or no selection).  For ROW 1 and 2 the
+// host passes the leaf's slot (pool + hsx * pool_stride) in the preloaded argument src_slot and the
+// row size in 16-byte units in ppk's top bits: wave 2 issues the row's loads at its first instruction.
 template <int NC, bool SEL, int ROW>
 __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy, const float *beta, const float *reward,
                                                 const float *value, int ppk, int bak, int hsx, float discount,
-                                                ChainIO io) {
-    static_assert(NC >= kWave && NC % kWave == 0, "k_chain3 node classes are whole waves");
+                                                const char *src_slot, ChainIO io) {
+    static_assert(NC >= kWave && NC % kWave == 0 && NC < 1024, "k_chain3 node classes are whole waves, < 1024");
     (void)io;  // (read through the kernel-argument pointer, see above)
     constexpr int NCH = NC / kWave;  // node chunks of one wave
     constexpr Chain3Layout<NC> L(NC);
-    const int P = ppk & 0xffff, PS = (int)((unsigned)ppk >> 16);
+    const int P = ppk & 0x3ff, PS = (ppk >> 10) & 0x3ff;
     const int A = (bak >> 24) & 0x7f, fast_ok = (int)((unsigned)bak >> 31);
     const int B = bak & 0xffffff;
     Dev d;
@@ -3275,7 +3283,26 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         // ======== wave 2: the leaf-row gather and the counters ========
         // Straight-line code in issue order (the row class ROW is a template argument): every wait
         // the compiler places then counts exactly the loads issued after the one it needs.
-        // (one scalar round trip: the outputs' kernel arguments, the header, the handle's constants)
+        // The row of this launch's leaf (hidden_state_index_x = hsx) is issued first, from preloaded
+        // arguments only (ROW 1, 2); then one scalar round trip: the outputs' kernel arguments, the
+        // header, the handle's constants.  This wave takes no barrier: nothing it does is read by
+        // another wave, and s_barrier waits only for the workgroup's waves that have not ended.
+        const long long o = (long long)l * 16;
+        unsigned char *sbig = smem + L.total;  // (ROW 2: 16 KiB past the layout)
+        int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
+        if constexpr (ROW == 1 || ROW == 2) {
+            const long long rb = (long long)((unsigned)ppk >> 20) * 16, lst = rb - 16;
+            const char *srow = (const char *)(const gchar *)src_slot + (long long)t * rb;
+            if constexpr (ROW == 1) {  // up to 4 KiB: four 16-byte registers per lane, offsets clamped into the row
+                gv0 = *(const int4 *)(srow + (o < lst ? o : lst));
+                gv1 = *(const int4 *)(srow + (o + 1024 < lst ? o + 1024 : lst));
+                gv2 = *(const int4 *)(srow + (o + 2048 < lst ? o + 2048 : lst));
+                gv3 = *(const int4 *)(srow + (o + 3072 < lst ? o + 3072 : lst));
+            } else {  // up to 16 KiB: sixteen LDS-DMA chunks of 1 KiB
+#pragma unroll
+                for (int k = 0; k < 16; ++k) glds16a(srow + (o + 1024 * k < lst ? o + 1024 * k : lst), sbig + 1024 * k);
+            }
+        }
         int8v io8 = sload8((const void *)iop);  // pool, pool_stride, row_bytes, gather_out
         int8v hv = sload8(hp);                  // cursor, tot, D, err, mm_min, mm_max, mm_cnt, leaf
         int rv0 = sload1(&d.A()[nb].x), omri = sload1(&pl->g.one_minus_rho), osti = sload1(&pl->d.o_stats);
@@ -3289,20 +3316,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         const int toth = hv[1], D = hv[2], herr = hv[3], leafh = hv[7];
         const int root_vis0 = rv0;
         const float omr = i2f(omri);
-        // the row of this launch's leaf (hidden_state_index_x = hsx), issued first
-        const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;
-        const long long last = row_bytes - 16, o = (long long)l * 16;
-        unsigned char *sbig = smem + L.total;  // (ROW 2: 16 KiB past the layout)
-        int4 gv0 = make_int4(0, 0, 0, 0), gv1 = gv0, gv2 = gv0, gv3 = gv0;
-        if constexpr (ROW == 1) {  // up to 4 KiB: four 16-byte registers per lane, offsets clamped into the row
-            gv0 = *(const int4 *)(src + (o < last ? o : last));
-            gv1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
-            gv2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
-            gv3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
-        } else if constexpr (ROW == 2) {  // up to 16 KiB: sixteen LDS-DMA chunks of 1 KiB
-#pragma unroll
-            for (int k = 0; k < 16; ++k) glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
-        }
+        const char *src = pool + (long long)hsx * pool_stride + (long long)t * row_bytes;  // (ROW 0)
         d.o_stats = (unsigned)osti;
         long long *st = d.stats() + (size_t)t * MZ_S_COUNT;
         const long long st_old = st[l < MZ_S_CYC_HEADER ? l : 0];
@@ -3318,7 +3332,6 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         if (SEL && Ds + 1 > PS) err |= kErrPath;
         if (SEL && !err && root_vis0 >= PS) err |= kErrTable;  // the root's child visits index the pUCT table
         stamp(ts, 2);
-        lds_barrier();  // (early: waves 0 and 1 must not wait for this wave's row)
         stamp(ts, 3);
         stamp(ts, 4);
         if (SEL && ROW != 3 && !err) {
@@ -3343,8 +3356,8 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         stamp(ts, 5);
         if (MZ_STAMPS && l == 0) {  // (wave 2's phases, stamped builds: slots wave 0 leaves alone)
             st[MZ_S_CYC_STAGE1] += (long long)(ts[1] - ts[0]);  // scalar round trip
-            st[MZ_S_CYC_STAGE2] += (long long)(ts[2] - ts[0]);  // arrival at the barrier
-            st[MZ_S_CYC_GATHER] += (long long)(ts[4] - ts[0]);  // engine words landed (after the barrier)
+            st[MZ_S_CYC_STAGE2] += (long long)(ts[2] - ts[0]);  // header checks done
+            st[MZ_S_CYC_GATHER] += (long long)(ts[4] - ts[0]);  // (the same point: no barrier)
             st[MZ_S_CYC_W1_STAGE2] += (long long)(ts[5] - ts[0]);  // row stored
         }
         if (l < MZ_S_CYC_HEADER) {
@@ -5218,13 +5231,16 @@ struct mz_batch {
     Geo geo;
     Dev dev;
     hipStream_t stream = nullptr;
-    hipEvent_t order_ev = nullptr;  // orders the old stream's work before the new one's (mz_set_stream)
+    hipEvent_t order_ev = nullptr;  // recorded after the last eager work the handle enqueued (mz_set_stream)
+    bool order_live = false;        // order_ev marks work that may still be running
+    bool dirty = false;             // work enqueued by the current call (OrderMark records order_ev)
     std::vector<void *> allocs;
+    size_t arena_bytes = 0;
     float *in_dev = nullptr;  // host-input staging [B*(2+3A)]
     int *sel_dev = nullptr;   // select output staging [3B]
     int *rb_dev = nullptr;    // packed readback
     size_t rb_words = 0;
-    std::vector<int> rb_host;
+    int *rb_host = nullptr;     // packed readback, host mirror (in the pinned stage)
     bool rb_valid = false;      // rb_host mirrors the current tree state
     bool rb_dev_valid = false;  // rb_dev mirrors the current tree state
     float rb_disc = 0.f;
@@ -5238,6 +5254,21 @@ struct mz_batch {
     int chain3_nc = 0;         // k_chain3 node class (64 .. 1024) for K = 1 trees, 0: k_chain / k_step
     int tree_nc = -1;          // k_tree node class for 2 <= K <= 64 trees (-1: k_step)
     Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
+    // Host-memory path (the cytree numpy surface): one pinned stage per handle, laid out
+    // [inputs B*(2+3NA) | selection B*(2+N) | error word | packed readback rb_words] (4-byte words).
+    // Inputs are packed into it on the host and go to the device in one copy; a host-memory
+    // expansion is only staged (`pend`) and launched with the next call -- fused with the selection
+    // when that call is batch_selection, as the reference driver's loop always does.
+    char *stage = nullptr;
+    size_t stage_bytes = 0;
+    float *st_in = nullptr;
+    int32_t *st_sel = nullptr;
+    int32_t *st_err = nullptr;
+    hipEvent_t st_ev = nullptr;  // the last copy out of st_in has been read when this fires
+    bool st_busy = false;
+    bool pend = false;           // a staged host-memory expansion not launched yet
+    int pend_hsx = 0, pend_K = 0;
+    float pend_disc = 0.f;
 };
 
 namespace {
@@ -5272,6 +5303,49 @@ const char *err_message(int bits) {
     return "device-side search error";
 }
 
+// Process-wide caches of released device arenas and pinned stages, reused by size: the
+// reference builds a new Tree_batch per search (mcts_sampled.py:89), and hipFree synchronises the
+// whole device while hipHostMalloc costs tens of microseconds.  Bounded; the rest is freed.
+struct BlockCache {
+    struct Blk {
+        int device;
+        size_t bytes;
+        void *p;
+    };
+    std::mutex mu;
+    std::vector<Blk> free;
+    size_t held = 0;
+    void *take(int device, size_t bytes) {
+        std::lock_guard<std::mutex> g(mu);
+        for (size_t i = 0; i < free.size(); ++i)
+            if (free[i].device == device && free[i].bytes == bytes) {
+                void *p = free[i].p;
+                held -= bytes;
+                free.erase(free.begin() + (long)i);
+                return p;
+            }
+        return nullptr;
+    }
+    // true: kept (the caller must not free it)
+    bool give(int device, size_t bytes, void *p, size_t cap_bytes, size_t cap_blocks) {
+        std::lock_guard<std::mutex> g(mu);
+        if (held + bytes > cap_bytes || free.size() >= cap_blocks) return false;
+        free.push_back({device, bytes, p});
+        held += bytes;
+        return true;
+    }
+};
+BlockCache &arena_cache() {
+    static BlockCache *c = new BlockCache;  // never destroyed: handles may outlive static teardown
+    return *c;
+}
+BlockCache &stage_cache() {
+    static BlockCache *c = new BlockCache;
+    return *c;
+}
+constexpr size_t kArenaCacheBytes = (size_t)4 << 30, kArenaCacheBlocks = 16;
+constexpr size_t kStageCacheBytes = (size_t)256 << 20, kStageCacheBlocks = 32;
+
 int ensure_device(mz_batch *b) {
     int cur = -1;
     HIP_TRY(hipGetDevice(&cur));
@@ -5280,10 +5354,15 @@ int ensure_device(mz_batch *b) {
 }
 
 // Poll the handle's error word (synchronises the stream).
+int ensure_stage(mz_batch *b);
 int check_device_errors(mz_batch *b) {
-    int e = 0;
-    HIP_TRY(hipMemcpyAsync(&e, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
+    int rc = ensure_stage(b);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    b->st_busy = false;  // (every copy out of the stage has completed)
+    b->dirty = b->order_live = false;  // nothing of this handle is in flight
+    const int e = *b->st_err;
     if (e) {
         char bits[32];
         std::snprintf(bits, sizeof bits, " (device error word 0x%x)", (unsigned)e);
@@ -5349,9 +5428,10 @@ struct ArenaPlan {
     }
     int allocate(mz_batch *b, Dev &d) {
         if (total / 256 > 0xffffffffull) return fail(MZ_ERR_UNSUPPORTED, "device arena larger than 1 TiB");
-        void *q = nullptr;
-        HIP_TRY(hipMalloc(&q, total));
+        void *q = arena_cache().take(b->device, total);
+        if (!q) HIP_TRY(hipMalloc(&q, total));
         b->allocs.push_back(q);
+        b->arena_bytes = total;
         d.base = (gchar *)q;
         for (auto &r : req) {
             if (r.off) *r.off = (unsigned)(r.at / 256);
@@ -5403,11 +5483,15 @@ void launch_chain3_row(mz_batch *b, const StepArgs &a) {
     const Dev &dv = b->dev;
     // (the first 14 argument dwords, through the discount, arrive preloaded in SGPRs)
     const ChainIO io{a.pool, a.pool_stride, a.row_bytes, a.gather_out, a.idx_x, a.idy, a.act};
+    // ROW 1, 2: the leaf's slot and the row size (16-byte units, <= 1024) ride in preloaded arguments
+    const bool pre = ROW == 1 || ROW == 2;
+    const char *src_slot = pre ? a.pool + (long long)a.hsx * a.pool_stride : nullptr;
+    const int rb16 = pre ? (int)(a.row_bytes / 16) : 0;
     hipLaunchKernelGGL((k_chain3<NC, SEL, ROW>), dim3(g.B), dim3(3 * kWave),
                        chain3_lds_bytes(NC) + (ROW == 2 ? 16 * 16 * kWave : 0), b->stream, (char *)dv.base, a.policy,
-                       a.beta, a.reward, a.value, g.P | (g.PS << 16),
+                       a.beta, a.reward, a.value, g.P | (g.PS << 10) | (rb16 << 20),
                        (int)((unsigned)g.B | ((unsigned)g.A << 24) | ((unsigned)b->fast_ok << 31)), a.hsx, a.discount,
-                       io);
+                       src_slot, io);
 }
 // the row class of a launch (k_chain3's ROW)
 int chain3_row(const StepArgs &a, bool sel) {
@@ -5450,6 +5534,7 @@ void launch_tree(mz_batch *b, const StepArgs &a) {
 
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
+    b->dirty = true;
     if (eb && b->chain3_nc > 0) {  // K = 1 trees: the three-wave chain kernel
         if (sel) {
             switch (b->chain3_nc) {
@@ -5571,8 +5656,108 @@ size_t rb_field_base(const mz_batch *b, int field) {
 size_t rb_field_width(const mz_batch *b, int field) { return (size_t)b->Wd * (field == MZ_F_ACTIONS ? b->N : 1); }
 
 
+// Every public call that enqueues work on the handle's stream ends by recording order_ev behind it
+// (OrderMark), so that mz_set_stream orders a new stream after that work without ever touching the
+// old stream, which the caller may have destroyed since.  Work recorded into a graph capture is
+// ordered by the capture (nothing to mark); a synchronisation leaves nothing to order.
+void mark_order(mz_batch *b) {
+    if (!b->dirty) return;
+    b->dirty = false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(b->stream, &cs) != hipSuccess) {  // (the stream of this very call)
+        (void)hipGetLastError();
+        return;
+    }
+    if (cs != hipStreamCaptureStatusNone) return;
+    if (!b->order_ev && hipEventCreateWithFlags(&b->order_ev, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(b->order_ev, b->stream) == hipSuccess) b->order_live = true;
+}
+struct OrderMark {
+    mz_batch *b;
+    ~OrderMark() {
+        if (b) mark_order(b);
+    }
+};
+
+// --- the host-memory path's pinned stage ------------------------------------------------------
+size_t stage_in_words(const mz_batch *b) { return (size_t)b->B * (2 + 3 * (size_t)b->NA); }
+size_t stage_sel_words(const mz_batch *b) { return (size_t)b->B * (2 + (size_t)b->N); }
+
+int ensure_stage(mz_batch *b) {
+    if (b->stage) return MZ_OK;
+    auto r64 = [](size_t w) { return (w + 15) & ~(size_t)15; };  // 64-byte aligned sections
+    const size_t w_in = r64(stage_in_words(b)), w_sel = r64(stage_sel_words(b)), w_err = 16, w_rb = r64(b->rb_words);
+    const size_t bytes = 4 * (w_in + w_sel + w_err + w_rb);
+    void *p = stage_cache().take(-1, bytes);
+    if (!p) HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    b->stage = (char *)p;
+    b->stage_bytes = bytes;
+    b->st_in = (float *)p;
+    b->st_sel = (int32_t *)p + w_in;
+    b->st_err = (int32_t *)p + w_in + w_sel;
+    b->rb_host = (int *)p + w_in + w_sel + w_err;
+    if (!b->st_ev) HIP_TRY(hipEventCreateWithFlags(&b->st_ev, hipEventDisableTiming));
+    return MZ_OK;
+}
+
+// st_in may be rewritten: the previous copy out of it has been read
+int stage_wait(mz_batch *b) {
+    int rc = ensure_stage(b);
+    if (rc) return rc;
+    if (b->st_busy) {
+        HIP_TRY(hipEventSynchronize(b->st_ev));
+        b->st_busy = false;
+    }
+    return MZ_OK;
+}
+
+// the first `words` of st_in -> in_dev, one copy on the handle's stream
+int stage_upload(mz_batch *b, size_t words) {
+    HIP_TRY(hipMemcpyAsync(b->in_dev, b->st_in, 4 * words, hipMemcpyHostToDevice, b->stream));
+    HIP_TRY(hipEventRecord(b->st_ev, b->stream));
+    b->st_busy = true;
+    b->dirty = true;
+    return MZ_OK;
+}
+
+// host arrays -> st_in in in_dev's layout [rewards B | values B | policy B*NA | beta B*NA (| noises B*NA)]
+void stage_pack(mz_batch *b, const float *rewards, const float *values, const float *policy, const float *beta,
+                const float *noises) {
+    const size_t B = b->B, NA = (size_t)b->NA;
+    float *p = b->st_in;
+    std::memcpy(p, rewards, 4 * B);
+    std::memcpy(p + B, values, 4 * B);
+    std::memcpy(p + 2 * B, policy, 4 * B * NA);
+    std::memcpy(p + 2 * B + B * NA, beta, 4 * B * NA);
+    if (noises) std::memcpy(p + 2 * B + 2 * B * NA, noises, 4 * B * NA);
+}
+
+StepArgs staged_expand_args(mz_batch *b) {
+    const size_t B = b->B, NA = (size_t)b->NA;
+    StepArgs a{};
+    a.hsx = b->pend_hsx;
+    a.discount = b->pend_disc;
+    a.K = b->pend_K;
+    a.reward = b->in_dev;
+    a.value = b->in_dev + B;
+    a.policy = b->in_dev + 2 * B;
+    a.beta = b->in_dev + 2 * B + B * NA;
+    return a;
+}
+
+// Launch a staged host-memory expansion on its own (every call but batch_selection, which fuses it).
+int flush_pending(mz_batch *b) {
+    if (!b->pend) return MZ_OK;
+    b->pend = false;
+    int rc = stage_upload(b, 2 * (size_t)b->B * (1 + (size_t)b->NA));
+    if (rc) return rc;
+    return launch_step(b, true, false, staged_expand_args(b));
+}
+
 // Packed readback computed on the device (stream-ordered, no synchronisation).
 int readback_dev(mz_batch *b, float disc) {
+    int rc = flush_pending(b);
+    if (rc) return rc;
     if (b->rb_dev_valid && b->rb_disc == disc) return MZ_OK;
     RbPtrs o;
     int *rb = b->rb_dev;
@@ -5582,6 +5767,7 @@ int readback_dev(mz_batch *b, float disc) {
     o.mp = (float *)(rb + b->B + n);
     o.deg = rb + rb_deg_base(b);
     for (int f = 0; f < MZ_F_COUNT; ++f) o.f[f] = rb + rb_field_base(b, f);
+    b->dirty = true;
     hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, disc, b->Wd, o);
     HIP_TRY(hipGetLastError());
     b->rb_dev_valid = true;
@@ -5592,6 +5778,7 @@ int readback_dev(mz_batch *b, float disc) {
 
 int copy_words(mz_batch *b, void *dst, const int *src, size_t n) {
     if (n == 0) return MZ_OK;
+    b->dirty = true;
     hipLaunchKernelGGL(k_copy_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, b->stream, (int *)dst, src, (int)n);
     HIP_TRY(hipGetLastError());
     return MZ_OK;
@@ -5602,8 +5789,9 @@ int readback(mz_batch *b, float disc) {
     if (b->rb_valid && b->rb_disc == disc) return MZ_OK;
     int rc = readback_dev(b, disc);
     if (rc) return rc;
-    b->rb_host.resize(b->rb_words);
-    HIP_TRY(hipMemcpyAsync(b->rb_host.data(), b->rb_dev, sizeof(int) * b->rb_words, hipMemcpyDeviceToHost, b->stream));
+    rc = ensure_stage(b);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(b->rb_host, b->rb_dev, sizeof(int) * b->rb_words, hipMemcpyDeviceToHost, b->stream));
     rc = check_device_errors(b);
     if (rc) return rc;
     b->rb_valid = true;
@@ -5631,8 +5819,23 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
                                          "agent_num <= 64 and agent_num * action_space_size <= 4096");
     if (S > 65000) return fail(MZ_ERR_UNSUPPORTED, "simulation_num > 65000");
     if (K > 4096) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 4096");
-    if ((long long)B * K * (S + 2) > 0xffffffffll)  // arena_hot's 32-bit offsets (> 256 GiB of node records)
-        return fail(MZ_ERR_UNSUPPORTED, "root_num * sampled_times * (simulation_num + 2) >= 2^32 nodes");
+    // max degree of any node: min(K, A^N) (children are the distinct sampled joint actions,
+    // cnode.cpp:242-294)
+    int Wd = 1;
+    {
+        long long an = 1;
+        for (int i = 0; i < N && an < K; ++i) an *= A;
+        Wd = (int)(K < an ? K : an);
+        if (Wd < 1) Wd = 1;
+    }
+    // Node pool per tree: the nodes a search can create, the root and at most Wd children for each of
+    // the S + 1 expansions (prepare + one per simulation).  The reference allocates K * (S + 2)
+    // (cnode.cpp:562); sizing by what is reachable picks the smallest layout class (3m K = 10:
+    // 460 nodes, not 1,040).  More expansions than simulation_num are refused either way (the
+    // engine stream and value-entry capacity are sized for S).
+    const long long P = 1 + (long long)Wd * (S + 1);
+    if ((long long)B * P > 0xffffffffll)  // arena_hot's 32-bit offsets (> 256 GiB of node records)
+        return fail(MZ_ERR_UNSUPPORTED, "root_num * (1 + min(K, A^N) * (simulation_num + 1)) >= 2^32 nodes");
     auto *b = new mz_batch;
     b->B = B;
     b->N = N;
@@ -5640,15 +5843,10 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     b->NA = N * A;
     b->K = K;
     b->S = S;
-    b->P = K * (S + 2);
+    b->P = (int)P;
     b->E = S + 1;
     b->PS = S + 2;
-    {  // max root degree: min(K, A^N)
-        long long an = 1;
-        for (int i = 0; i < N && an < K; ++i) an *= A;
-        b->Wd = (int)(K < an ? K : an);
-    }
-    if (b->Wd < 1) b->Wd = 1;
+    b->Wd = Wd;
     // RNG words a search can consume: 2KN per expansion (S+1 of them, +1 slack) and at most
     // (leaf depth) words per selection, sum_{s<=S} (s+1); rounded up to whole 624-word blocks.
     {
@@ -5742,7 +5940,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     }
     if (g.lds > 160 * 1024) {
         delete b;
-        return fail(MZ_ERR_UNSUPPORTED, "tree too large for the LDS-resident kernels (K*(S+2) nodes)");
+        return fail(MZ_ERR_UNSUPPORTED, "tree too large for the LDS-resident kernels (1 + min(K, A^N)*(S+1) nodes)");
     }
     if (K == 1 && N == 1 && !getenv_flag("MZ_NO_CHAIN")) {
         b->chain_nc = 0;
@@ -5807,9 +6005,9 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         mz_destroy(b);
         return fail(MZ_ERR_DEVICE, m);
     }
-    // k_chain3 takes P and PS in 16 bits each (K = 1 pools of <= 1024 nodes always fit)
+    // k_chain3 takes P and PS in 10 bits each (its pools have <= 256 nodes)
     // (pools above 256 nodes keep k_chain: wave 1 holds the chain's records in registers, 8 per 64 nodes)
-    if (b->chain_nc > 0 && b->chain_nc <= 256 && b->P < 65536 && b->PS < 65536 && !getenv_flag("MZ_CHAIN_V2"))
+    if (b->chain_nc > 0 && b->chain_nc <= 256 && b->P < 1024 && b->PS < 1024 && !getenv_flag("MZ_CHAIN_V2"))
         b->chain3_nc = b->chain_nc;
     const Params host_params{b->geo, b->dev};
     std::vector<float> lp(b->PS + 1 + kWave, 0.f);
@@ -5873,8 +6071,14 @@ int mz_destroy(mz_batch *b) {
     if (!b) return MZ_OK;
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     else (void)hipDeviceSynchronize();
-    for (void *p : b->allocs) (void)hipFree(p);
+    // (a staged host-memory expansion nobody reads any more is dropped)
+    for (void *p : b->allocs)
+        if (!(b->arena_bytes && arena_cache().give(b->device, b->arena_bytes, p, kArenaCacheBytes, kArenaCacheBlocks)))
+            (void)hipFree(p);
+    if (b->stage && !stage_cache().give(-1, b->stage_bytes, b->stage, kStageCacheBytes, kStageCacheBlocks))
+        (void)hipHostFree(b->stage);
     if (b->order_ev) (void)hipEventDestroy(b->order_ev);
+    if (b->st_ev) (void)hipEventDestroy(b->st_ev);
     delete b;
     return MZ_OK;
 }
@@ -5885,30 +6089,27 @@ int mz_set_stream(mz_batch *b, void *stream) {
     if (ns == b->stream) return MZ_OK;
     int rc = ensure_device(b);
     if (rc) return rc;
-    // the new stream waits for the work already queued on the old one (the handle's calls stay in
-    // order), except across a graph capture boundary, where the capture itself orders nothing and
-    // an event from outside the capture may not be waited on.  An old stream the runtime no longer
-    // knows (the caller destroyed it: its work was handed to the runtime to finish and the caller
-    // ordered nothing after it) has nothing to order: its error is cleared and the handle switches.
-    hipStreamCaptureStatus co = hipStreamCaptureStatusNone, cn = hipStreamCaptureStatusNone;
+    rc = flush_pending(b);  // (on the old stream, ordered before the new one's work below)
+    mark_order(b);
+    if (rc) return rc;
+    // The new stream waits for the eager work the handle enqueued last (order_ev, recorded behind it
+    // by that call): the old stream itself is never queried, so one the caller has destroyed since is
+    // harmless.  Not across a graph-capture boundary: a capture orders nothing outside it and may not
+    // wait on an event recorded outside it.
+    hipStreamCaptureStatus cn = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(ns, &cn));
-    bool old_alive = true;
-    if (hipStreamIsCapturing(b->stream, &co) != hipSuccess) {
-        (void)hipGetLastError();
-        old_alive = false;
-    }
-    if (old_alive && co == hipStreamCaptureStatusNone && cn == hipStreamCaptureStatusNone) {
-        if (!b->order_ev) HIP_TRY(hipEventCreateWithFlags(&b->order_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(b->order_ev, b->stream));
-        HIP_TRY(hipStreamWaitEvent(ns, b->order_ev, 0));
-    }
+    if (b->order_live && cn == hipStreamCaptureStatusNone) HIP_TRY(hipStreamWaitEvent(ns, b->order_ev, 0));
+    b->order_live = false;
     b->stream = ns;
     return MZ_OK;
 }
 
 int mz_synchronize(mz_batch *b) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
     if (rc) return rc;
     return check_device_errors(b);
 }
@@ -5916,18 +6117,21 @@ int mz_synchronize(mz_batch *b) {
 int mz_prepare(mz_batch *b, const float *rewards, const float *values, const float *policy, const float *beta, int K,
                float noise_eps, const float *noises, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
     int rc = ensure_device(b);
     if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
     const size_t B = b->B, NA = (size_t)b->NA;
     PrepArgs a;
-    if (mem == MZ_MEM_HOST) {
+    if (mem == MZ_MEM_HOST) {  // one copy out of the pinned stage
+        rc = stage_wait(b);
+        if (rc) return rc;
+        stage_pack(b, rewards, values, policy, beta, noises);
+        rc = stage_upload(b, stage_in_words(b));
+        if (rc) return rc;
         float *p = b->in_dev;
-        HIP_TRY(hipMemcpyAsync(p, rewards, 4 * B, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + B, values, 4 * B, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + 2 * B, policy, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + 2 * B + B * NA, beta, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + 2 * B + 2 * B * NA, noises, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
         a.reward = p;
         a.value = p + B;
         a.policy = p + 2 * B;
@@ -5946,6 +6150,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
     a.K = K;
     a.idx_x = a.idy = a.act = nullptr;
     const size_t jl = (b->N > 1) ? (size_t)((12 * b->NA + 15) & ~15) + 8 * (size_t)b->NA + 4 * (size_t)kWave * b->N : 0;
+    b->dirty = true;
     hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), jl, b->stream, b->prm, a);
     HIP_TRY(hipGetLastError());
     b->rb_valid = b->rb_dev_valid = false;
@@ -5959,6 +6164,7 @@ int mz_prepare_select(mz_batch *b, const float *rewards, const float *values, co
                       int K, float noise_eps, const float *noises, float c2, float c1, float discount, int32_t *idx_x,
                       int32_t *idy, int32_t *actions) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
     if (!idx_x || !idy || !actions) return fail(MZ_ERR_ARG, "null selection output");
     if (b->N > 1) {  // joint-action trees: the two calls
@@ -5967,6 +6173,8 @@ int mz_prepare_select(mz_batch *b, const float *rewards, const float *values, co
         return mz_select(b, c2, c1, discount, idx_x, idy, actions, MZ_MEM_DEVICE);
     }
     int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
     if (rc) return rc;
     rc = ensure_tables(b, c2, c1);  // (for the launches that follow; the first selection needs none)
     if (rc) return rc;
@@ -5981,6 +6189,7 @@ int mz_prepare_select(mz_batch *b, const float *rewards, const float *values, co
     a.idx_x = idx_x;
     a.idy = idy;
     a.act = actions;
+    b->dirty = true;
     hipLaunchKernelGGL(k_prepare, dim3(b->B), dim3(256), 0, b->stream, b->prm, a);
     HIP_TRY(hipGetLastError());
     b->rb_valid = b->rb_dev_valid = false;
@@ -5992,79 +6201,93 @@ int mz_prepare_select(mz_batch *b, const float *rewards, const float *values, co
 int mz_select(mz_batch *b, float c2, float c1, float discount, int32_t *idx_x, int32_t *idy, int32_t *actions,
               int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (!b->prepared) return fail(MZ_ERR_RUNTIME, "batch_selection before prepare");
     int rc = ensure_device(b);
     if (rc) return rc;
     rc = ensure_tables(b, c2, c1);
     if (rc) return rc;
+    if (mem != MZ_MEM_HOST && mem != MZ_MEM_DEVICE) return fail(MZ_ERR_ARG, "bad memory kind");
+    const bool fuse = mem == MZ_MEM_HOST && b->pend;  // the staged expansion + this selection, one launch
+    if (!fuse) {
+        rc = flush_pending(b);
+        if (rc) return rc;
+    }
     StepArgs a{};
+    if (fuse) {
+        b->pend = false;
+        rc = stage_upload(b, 2 * (size_t)b->B * (1 + (size_t)b->NA));
+        if (rc) return rc;
+        a = staged_expand_args(b);
+    }
     a.discount = discount;
     if (mem == MZ_MEM_HOST) {
         a.idx_x = b->sel_dev;
         a.idy = b->sel_dev + b->B;
         a.act = b->sel_dev + 2 * b->B;
-    } else if (mem == MZ_MEM_DEVICE) {
+    } else {
         a.idx_x = idx_x;
         a.idy = idy;
         a.act = actions;
-    } else {
-        return fail(MZ_ERR_ARG, "bad memory kind");
     }
-    rc = launch_step(b, false, true, a);
+    rc = launch_step(b, fuse, true, a);
     if (rc) return rc;
-    if (mem == MZ_MEM_HOST) {
-        std::vector<int32_t> tmp((size_t)b->B * (2 + b->N));
-        HIP_TRY(hipMemcpyAsync(tmp.data(), b->sel_dev, sizeof(int32_t) * tmp.size(), hipMemcpyDeviceToHost, b->stream));
+    if (mem == MZ_MEM_HOST) {  // selection + error word into the pinned stage, one synchronisation
+        rc = ensure_stage(b);
+        if (rc) return rc;
+        const size_t n = stage_sel_words(b);
+        HIP_TRY(hipMemcpyAsync(b->st_sel, b->sel_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost, b->stream));
         rc = check_device_errors(b);
         if (rc) return rc;
-        std::memcpy(idx_x, tmp.data(), sizeof(int32_t) * b->B);
-        std::memcpy(idy, tmp.data() + b->B, sizeof(int32_t) * b->B);
-        std::memcpy(actions, tmp.data() + 2 * b->B, sizeof(int32_t) * b->B * b->N);
+        std::memcpy(idx_x, b->st_sel, sizeof(int32_t) * b->B);
+        std::memcpy(idy, b->st_sel + b->B, sizeof(int32_t) * b->B);
+        std::memcpy(actions, b->st_sel + 2 * b->B, sizeof(int32_t) * b->B * b->N);
     }
     return MZ_OK;
 }
 
+// device-memory inputs of an expansion (host-memory ones go through the pinned stage)
 static int expand_inputs(mz_batch *b, const float *rewards, const float *values, const float *policy,
-                         const float *beta, int mem, StepArgs &a) {
-    const size_t B = b->B, NA = (size_t)b->NA;
-    if (mem == MZ_MEM_HOST) {
-        float *p = b->in_dev;
-        HIP_TRY(hipMemcpyAsync(p, rewards, 4 * B, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + B, values, 4 * B, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + 2 * B, policy, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
-        HIP_TRY(hipMemcpyAsync(p + 2 * B + B * NA, beta, 4 * B * NA, hipMemcpyHostToDevice, b->stream));
-        a.reward = p;
-        a.value = p + B;
-        a.policy = p + 2 * B;
-        a.beta = p + 2 * B + B * NA;
-    } else if (mem == MZ_MEM_DEVICE) {
-        a.reward = rewards;
-        a.value = values;
-        a.policy = policy;
-        a.beta = beta;
-    } else {
-        return fail(MZ_ERR_ARG, "bad memory kind");
-    }
+                         const float *beta, StepArgs &a) {
+    (void)b;
+    a.reward = rewards;
+    a.value = values;
+    a.policy = policy;
+    a.beta = beta;
     return MZ_OK;
 }
 
 int mz_expand_backup(mz_batch *b, int hsx, float discount, int K, const float *rewards, const float *values,
                      const float *policy, const float *beta, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (!b->prepared) return fail(MZ_ERR_RUNTIME, "batch_expansion_and_backup before prepare");
     if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
+    if (mem != MZ_MEM_HOST && mem != MZ_MEM_DEVICE) return fail(MZ_ERR_ARG, "bad memory kind");
     int rc = ensure_device(b);
     if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
+    if (mem == MZ_MEM_HOST) {
+        // staged in pinned memory; launched by the next call (with batch_selection: one fused
+        // launch).  Its device-side errors surface at that call.
+        rc = stage_wait(b);
+        if (rc) return rc;
+        stage_pack(b, rewards, values, policy, beta, nullptr);
+        b->pend = true;
+        b->pend_hsx = hsx;
+        b->pend_disc = discount;
+        b->pend_K = K;
+        b->rb_valid = b->rb_dev_valid = false;
+        return MZ_OK;
+    }
     StepArgs a{};
     a.hsx = hsx;
     a.discount = discount;
     a.K = K;
-    rc = expand_inputs(b, rewards, values, policy, beta, mem, a);
+    rc = expand_inputs(b, rewards, values, policy, beta, a);
     if (rc) return rc;
-    rc = launch_step(b, true, false, a);
-    if (rc) return rc;
-    if (mem == MZ_MEM_HOST) return check_device_errors(b);
-    return MZ_OK;
+    return launch_step(b, true, false, a);
 }
 
 int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const float *rewards, const float *values,
@@ -6072,11 +6295,14 @@ int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const f
                             int32_t *actions, const void *pool, int64_t pool_slot_stride, int64_t row_bytes,
                             void *gather_out) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (!b->prepared) return fail(MZ_ERR_RUNTIME, "expansion before prepare");
     if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
     if (pool && (!gather_out || row_bytes <= 0 || (row_bytes & 3)))
         return fail(MZ_ERR_ARG, "gather needs an output buffer and row_bytes a positive multiple of 4");
     int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
     if (rc) return rc;
     rc = ensure_tables(b, c2, c1);
     if (rc) return rc;
@@ -6084,7 +6310,7 @@ int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const f
     a.hsx = hsx;
     a.discount = discount;
     a.K = K;
-    rc = expand_inputs(b, rewards, values, policy, beta, MZ_MEM_DEVICE, a);
+    rc = expand_inputs(b, rewards, values, policy, beta, a);
     if (rc) return rc;
     a.idx_x = idx_x;
     a.idy = idy;
@@ -6099,10 +6325,14 @@ int mz_expand_backup_select(mz_batch *b, int hsx, float discount, int K, const f
 // include/mzdriver.h
 int mz_reseed(mz_batch *b, uint32_t seed) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
     if (rc) return rc;
     b->geo.seed = seed;
     b->prepared = false;
+    b->dirty = true;
     hipLaunchKernelGGL(k_set_word, dim3(1), dim3(1), 0, b->stream, b->dev.seed(), (unsigned)seed);
     HIP_TRY(hipGetLastError());
     return MZ_OK;
@@ -6110,8 +6340,23 @@ int mz_reseed(mz_batch *b, uint32_t seed) {
 
 int mz_state_changed(mz_batch *b) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
+    int rc = flush_pending(b);
+    if (rc) return rc;
     b->rb_valid = b->rb_dev_valid = false;
     b->prepared = true;
+    return MZ_OK;
+}
+
+int mz_fused_kernel(mz_batch *b, char *out, int len) {
+    if (!b || !out || len < 1) return fail(MZ_ERR_ARG, "mz_fused_kernel: null argument");
+    char name[48];
+    if (b->chain3_nc > 0) std::snprintf(name, sizeof name, "k_chain3<%d>", b->chain3_nc);
+    else if (b->chain_nc >= 0) std::snprintf(name, sizeof name, "k_chain<%d>", b->chain_nc);
+    else if (b->tree_nc > 0) std::snprintf(name, sizeof name, "k_tree<%d>", b->tree_nc);
+    else if (b->N > 1) std::snprintf(name, sizeof name, "k_step<0,joint>");
+    else std::snprintf(name, sizeof name, "k_step<%d>", b->nc);
+    std::snprintf(out, (size_t)len, "%s", name);
     return MZ_OK;
 }
 
@@ -6122,6 +6367,8 @@ int mz_internal_launch_info(mz_batch *b, int *B, int *A, hipStream_t *stream) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
     int rc = ensure_device(b);
     if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
     *B = b->B;
     *A = b->A;
     *stream = b->stream;
@@ -6130,11 +6377,21 @@ int mz_internal_launch_info(mz_batch *b, int *B, int *A, hipStream_t *stream) {
 
 int mz_internal_agent_num(mz_batch *b) { return b ? b->N : 0; }
 
+void mz_internal_enqueued(mz_batch *b) {
+    if (!b) return;
+    b->dirty = true;
+    mark_order(b);
+}
+
 int mz_gather_rows(mz_batch *b, const void *pool, int64_t stride, int64_t row_bytes, const int32_t *idx_x, void *out) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (row_bytes <= 0 || (row_bytes & 3)) return fail(MZ_ERR_ARG, "row_bytes must be a positive multiple of 4");
     int rc = ensure_device(b);
     if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
+    b->dirty = true;
     hipLaunchKernelGGL(k_gather, dim3(b->B), dim3(kWave), 0, b->stream, (const char *)pool, (long long)stride,
                        (long long)row_bytes, (const int *)idx_x, (char *)out);
     HIP_TRY(hipGetLastError());
@@ -6143,8 +6400,11 @@ int mz_gather_rows(mz_batch *b, const void *pool, int64_t stride, int64_t row_by
 
 int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (!out) return fail(MZ_ERR_ARG, "null output list");
     int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
     if (rc) return rc;
     RbPtrs o;
     o.values = out->values;
@@ -6152,6 +6412,7 @@ int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out)
     o.mp = out->marginal_priors;
     o.deg = out->degrees;
     for (int f = 0; f < MZ_F_COUNT; ++f) o.f[f] = (int *)out->sampled[f];
+    b->dirty = true;
     hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, discount, b->Wd, o);
     HIP_TRY(hipGetLastError());
     return MZ_OK;
@@ -6159,6 +6420,7 @@ int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out)
 
 int mz_get_roots_values(mz_batch *b, float *out, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     int rc = ensure_device(b);
     if (rc) return rc;
     if (mem == MZ_MEM_DEVICE) {
@@ -6170,12 +6432,13 @@ int mz_get_roots_values(mz_batch *b, float *out, int mem) {
     }
     rc = readback(b, b->rb_valid ? b->rb_disc : 0.f);
     if (rc) return rc;
-    std::memcpy(out, b->rb_host.data(), 4 * (size_t)b->B);
+    std::memcpy(out, b->rb_host, 4 * (size_t)b->B);
     return MZ_OK;
 }
 
 int mz_get_roots_marginal_visit_count(mz_batch *b, int32_t *out, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     int rc = ensure_device(b);
     if (rc) return rc;
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
@@ -6187,12 +6450,13 @@ int mz_get_roots_marginal_visit_count(mz_batch *b, int32_t *out, int mem) {
         if (rc) return rc;
         return MZ_OK;
     }
-    std::memcpy(out, b->rb_host.data() + b->B, 4 * n);
+    std::memcpy(out, b->rb_host + b->B, 4 * n);
     return MZ_OK;
 }
 
 int mz_get_roots_marginal_priors(mz_batch *b, float *out, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     int rc = ensure_device(b);
     if (rc) return rc;
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
@@ -6204,7 +6468,7 @@ int mz_get_roots_marginal_priors(mz_batch *b, float *out, int mem) {
         if (rc) return rc;
         return MZ_OK;
     }
-    std::memcpy(out, b->rb_host.data() + b->B + n, 4 * n);
+    std::memcpy(out, b->rb_host + b->B + n, 4 * n);
     return MZ_OK;
 }
 
@@ -6235,12 +6499,13 @@ int mz_get_root_sampled(mz_batch *b, int field, int tree_id, float discount, voi
     if (rc) return rc;
     const int deg = b->rb_host[rb_deg_base(b) + tree_id];
     const size_t per = (field == MZ_F_ACTIONS) ? (size_t)b->N : 1;
-    std::memcpy(out, b->rb_host.data() + rb_field_base(b, field) + (size_t)tree_id * b->Wd * per, 4 * (size_t)deg * per);
+    std::memcpy(out, b->rb_host + rb_field_base(b, field) + (size_t)tree_id * b->Wd * per, 4 * (size_t)deg * per);
     return MZ_OK;
 }
 
 int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *out, int32_t *degrees, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
     if (field < 0 || field >= MZ_F_COUNT) return fail(MZ_ERR_ARG, "unknown field");
     int rc = ensure_device(b);
     if (rc) return rc;
@@ -6258,8 +6523,8 @@ int mz_get_roots_sampled_padded(mz_batch *b, int field, float discount, void *ou
         }
         return MZ_OK;
     }
-    std::memcpy(out, b->rb_host.data() + rb_field_base(b, field), 4 * n);
-    if (degrees) std::memcpy(degrees, b->rb_host.data() + dego, 4 * (size_t)b->B);
+    std::memcpy(out, b->rb_host + rb_field_base(b, field), 4 * n);
+    if (degrees) std::memcpy(degrees, b->rb_host + dego, 4 * (size_t)b->B);
     return MZ_OK;
 }
 
@@ -6324,6 +6589,8 @@ int mz_get_stats(mz_batch *b, int64_t *out) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
     int rc = ensure_device(b);
     if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
     std::vector<long long> st((size_t)b->B * MZ_S_COUNT);
     HIP_TRY(hipMemcpyAsync(st.data(), b->dev.stats(), sizeof(long long) * st.size(), hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
@@ -6336,6 +6603,8 @@ int mz_get_stats(mz_batch *b, int64_t *out) {
 int mz_print(mz_batch *b) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
     int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
     if (rc) return rc;
     std::vector<TreeHdr> h(b->B);
     HIP_TRY(hipMemcpyAsync(h.data(), b->dev.hdr(), sizeof(TreeHdr) * b->B, hipMemcpyDeviceToHost, b->stream));

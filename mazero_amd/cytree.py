@@ -34,7 +34,16 @@ def _is_device_tensor(x) -> bool:
     return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
 
 
+def _raw_stream_of(device: int) -> int:
+    """The handle of torch's current stream on `device` (what torch.cuda.current_stream(device)
+    .cuda_stream returns, without building a Stream object on every call)."""
+    f = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    return f(device) if f is not None else torch.cuda.current_stream(device).cuda_stream
+
+
 def _f32_host(x) -> np.ndarray:
+    if type(x) is np.ndarray and x.dtype == np.float32 and x.flags.c_contiguous:  # the common case
+        return x.reshape(-1)
     if torch is not None and isinstance(x, torch.Tensor):
         x = x.detach().cpu().numpy()
     x = np.asarray(x).reshape(-1)
@@ -52,16 +61,17 @@ def _f32_dev(x):
     return x.contiguous()
 
 
-def _check_out(t, numel: int, dtype, what: str) -> None:
+def _check_out(t, numel: int, dtype, what: str, device: int) -> None:
     """A caller-provided device output of a readback launch: the kernel writes `numel` elements of
     `dtype` from its data pointer, so anything smaller, of another dtype, strided or on another
-    device would be overwritten out of bounds.  None = field not requested."""
+    device than the tree's (`device`) would be overwritten out of bounds.  None = field not
+    requested."""
     if t is None:
         return
     if not isinstance(t, torch.Tensor) or not t.is_cuda:
         raise ValueError(f"{what}: a CUDA tensor is required")
-    if t.device.index != torch.cuda.current_device():
-        raise ValueError(f"{what}: on {t.device}, but the tree's device is cuda:{torch.cuda.current_device()}")
+    if t.device.index != device:
+        raise ValueError(f"{what}: on {t.device}, but the tree lives on cuda:{device}")
     if t.dtype != dtype:
         raise ValueError(f"{what}: dtype {t.dtype}, expected {dtype}")
     if not t.is_contiguous():
@@ -115,6 +125,8 @@ class Tree_batch:
         self._stream_ptr = None
         # device backends follow torch's current stream on every call (oracle libraries are host-only)
         self._on_device = torch is not None and lib.mz_backend() == b"hip-gfx950"
+        # the device the handle's arena lives on (mz_create allocates on the current device)
+        self.device_index = torch.cuda.current_device() if self._on_device else None
         self._maxdeg = None
 
     # -- lifetime ---------------------------------------------------------------------------
@@ -133,7 +145,7 @@ class Tree_batch:
         must finish before the tree is read)."""
         if not self._on_device:
             return
-        s = torch.cuda.current_stream().cuda_stream
+        s = _raw_stream_of(self.device_index)
         if s != self._stream_ptr:
             check(self._lib, self._lib.mz_set_stream(self._h, C.c_void_p(s)), "set_stream")
             self._stream_ptr = s
@@ -149,7 +161,7 @@ class Tree_batch:
             return [C.c_void_p(t.data_ptr()) for t in ts], MZ_MEM_DEVICE, ts
         hs = [_f32_host(a) for a in arrays]
         self._sync_stream()
-        return [h.ctypes.data_as(C.c_void_p) for h in hs], MZ_MEM_HOST, hs
+        return [h.ctypes.data for h in hs], MZ_MEM_HOST, hs
 
     # -- search (cytree.pyx:21-91) --------------------------------------------------------------
     def prepare(self, rewards, values, policy_probs, beta, sampled_times, noise_eps, noises):
@@ -162,22 +174,13 @@ class Tree_batch:
 
     def batch_selection(self, pb_c_base, pb_c_init, discount):
         B, N = self.root_num, self.agent_num
-        idx = np.empty(B, np.int32)
-        idy = np.empty(B, np.int32)
-        act = np.empty(B * N, np.int32)
+        out = np.empty((2 + N) * B, np.int32)  # idx | idy | actions, one buffer
+        p = out.ctypes.data
         self._sync_stream()
-        rc = self._lib.mz_select(
-            self._h,
-            float(pb_c_base),
-            float(pb_c_init),
-            float(discount),
-            idx.ctypes.data_as(C.c_void_p),
-            idy.ctypes.data_as(C.c_void_p),
-            act.ctypes.data_as(C.c_void_p),
-            MZ_MEM_HOST,
-        )
+        rc = self._lib.mz_select(self._h, float(pb_c_base), float(pb_c_init), float(discount), p, p + 4 * B,
+                                 p + 8 * B, MZ_MEM_HOST)
         check(self._lib, rc, "batch_selection")
-        return idx.tolist(), idy.tolist(), act.reshape(B, N)
+        return out[:B].tolist(), out[B:2 * B].tolist(), out[2 * B:].reshape(B, N)
 
     def batch_expansion_and_backup(self, hidden_state_index_x, discount, sampled_times, rewards, values,
                                    policy_probs, beta):
@@ -296,10 +299,11 @@ class Tree_batch:
         sampled {field name: [B, max_children(*N)]} as get_roots_sampled_padded_device lays them out."""
         B, NA = self.root_num, self.agent_num * self.action_space_size
         W = self.max_children() if sampled else 0
-        _check_out(values, B, torch.float32, "values")
-        _check_out(marginal_visit_count, B * NA, torch.int32, "marginal_visit_count")
-        _check_out(marginal_priors, B * NA, torch.float32, "marginal_priors")
-        _check_out(degrees, B, torch.int32, "degrees")
+        dv = self.device_index
+        _check_out(values, B, torch.float32, "values", dv)
+        _check_out(marginal_visit_count, B * NA, torch.int32, "marginal_visit_count", dv)
+        _check_out(marginal_priors, B * NA, torch.float32, "marginal_priors", dv)
+        _check_out(degrees, B, torch.int32, "degrees", dv)
         o = ReadbackOut()
         ptr = lambda x: None if x is None else x.data_ptr()  # noqa: E731
         o.values, o.marginal_visit_count = ptr(values), ptr(marginal_visit_count)
@@ -308,7 +312,7 @@ class Tree_batch:
             if name not in FIELDS:
                 raise ValueError(f"get_roots_device: unknown sampled field {name!r}")
             width = W * self.agent_num if name == "actions" else W
-            _check_out(t, B * width, torch.int32 if name in INT_FIELDS else torch.float32, f"sampled[{name!r}]")
+            _check_out(t, B * width, torch.int32 if name in INT_FIELDS else torch.float32, f"sampled[{name!r}]", dv)
             o.sampled[FIELDS[name]] = t.data_ptr()
         self._sync_stream()
         check(self._lib, self._lib.mz_get_roots_device(self._h, float(discount), C.byref(o)), "get_roots_device")
@@ -419,6 +423,13 @@ class Tree_batch:
         self._sync_stream()
         check(self._lib, self._lib.mz_get_stats(self._h, out), "stats")
         return dict(zip(_capi.STATS, list(out)))
+
+    def fused_kernel(self) -> str:
+        """Name of the kernel a fused simulation step launches on this handle (include/mzdriver.h
+        mz_fused_kernel; product library only)."""
+        buf = C.create_string_buffer(64)
+        check(self._lib, self._lib.mz_fused_kernel(self._h, buf, len(buf)), "fused_kernel")
+        return buf.value.decode()
 
     def synchronize(self):
         self._sync_stream()

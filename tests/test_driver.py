@@ -595,3 +595,32 @@ def test_device_driver_matches_reference_driver(path):
         np.testing.assert_array_equal(np.asarray(rng.random(4)), fx.z["rng_after"])
     loop = [v for v in _LOOPS.values() if v.model_ref() is net][0]
     assert isinstance(loop.graph, torch.cuda.CUDAGraph), "the third search did not replay a graph"
+
+
+@pytest.mark.gpu
+def test_graph_census_counts_child_graph_memsets():
+    """mz_graph_census recurses into child-graph nodes: a memset node nested one level down (as a
+    nested capture or an embedded graph records it) is counted, so such a search loop stays eager."""
+    import torch
+
+    from mazero_amd._capi import check
+    from mazero_amd._lib import load
+
+    class MemsetParams(C.Structure):  # hipMemsetParams (hip_runtime_api.h)
+        _fields_ = [("dst", C.c_void_p), ("elementSize", C.c_uint), ("height", C.c_size_t), ("pitch", C.c_size_t),
+                    ("value", C.c_uint), ("width", C.c_size_t)]
+
+    lib = load()
+    hip = C.CDLL("libamdhip64.so.7")
+    buf = torch.zeros(64, dtype=torch.int32, device="cuda")
+    child, parent, node, cnode = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+    assert hip.hipGraphCreate(C.byref(child), 0) == 0
+    assert hip.hipGraphCreate(C.byref(parent), 0) == 0
+    prm = MemsetParams(buf.data_ptr(), 4, 1, 0, 0, 64)
+    assert hip.hipGraphAddMemsetNode(C.byref(node), child, None, C.c_size_t(0), C.byref(prm)) == 0
+    assert hip.hipGraphAddChildGraphNode(C.byref(cnode), parent, None, C.c_size_t(0), child) == 0
+    total, memsets = C.c_int(0), C.c_int(0)
+    check(lib, lib.mz_graph_census(parent, C.byref(total), C.byref(memsets)), "graph_census")
+    assert (total.value, memsets.value) == (2, 1)
+    hip.hipGraphDestroy(parent)
+    hip.hipGraphDestroy(child)

@@ -101,6 +101,19 @@ def test_golden_host_path(gpu_lib, path):
 
 
 @pytest.mark.parametrize("path", TRACES, ids=IDS)
+def test_golden_host_path_fused(gpu_lib, path):
+    """The host-memory path as the reference driver calls it (batch_selection, then
+    batch_expansion_and_backup, no readback in between): each staged expansion is launched fused
+    with the next selection, one host->device and one device->host copy per simulation."""
+    from mazero_amd.synthetic import run_search
+
+    inp, knobs, K, expected = load_trace(path)
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    expected = {k: v for k, v in expected.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(run_search(tb, inp, K, knobs, per_sim=False), expected, "gpu(host, fused) ")
+
+
+@pytest.mark.parametrize("path", TRACES, ids=IDS)
 def test_golden_device_tensors(gpu_lib, path):
     from mazero_amd.synthetic import run_search
 
@@ -154,7 +167,18 @@ BIG = [
     # E = 101 k_tree
     ("k3_512_class_kstep", 64, 9, 3, 150, 0.0),
     ("k4_512_class_tree", 64, 9, 4, 100, 0.0),
+    # K = 1 pools above k_chain3's 256 nodes: k_chain<512> (S + 2 <= 512), k_chain<1024>, and the
+    # run-time layout k_chain<0> (S >= 1023)
+    ("k1_chain512", 64, 9, 1, 300, 0.3),
+    ("k1_chain1024", 32, 11, 1, 700, 0.0),
+    ("k1_chain_general", 16, 9, 1, 1100, 0.0),
 ]
+
+
+# the fused kernel each row exists for (mz_fused_kernel)
+BIG_KERNEL = {"3m_k1": "k_chain3<64>", "27m_k1": "k_chain3<256>", "k1_chain512": "k_chain<512>",
+              "k1_chain1024": "k_chain<1024>", "k1_chain_general": "k_chain<0>",
+              "27m_k8_general_layout": "k_step<0>", "k2_long_value_sets": "k_step<1024>"}
 
 
 @pytest.mark.parametrize("name,B,A,K,S,lz", BIG, ids=[b[0] for b in BIG])
@@ -165,7 +189,10 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     inp = make_search_inputs(rng, B, A, S, legal_zero_frac=lz)
     knobs = {}
     exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
-    out, _ = run_fused(make_tb(gpu_lib, inp, K, knobs), to_device(inp), K, knobs)
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    if name in BIG_KERNEL:
+        assert tb.fused_kernel() == BIG_KERNEL[name]
+    out, _ = run_fused(tb, to_device(inp), K, knobs)
     exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
     assert_same(out, exp, f"gpu {name} ")
     # size-independent properties (hold for the reference by construction)
@@ -176,6 +203,20 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert (deg >= 1).all() and (deg <= min(K, A)).all()
     bh = out["sampled_beta_hat"].sum(axis=1)
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
+
+
+def test_chain_v2_on_reference_fixture(gpu_lib, monkeypatch):
+    """MZ_CHAIN_V2=1 (read at mz_create) sends K = 1 pools of <= 256 nodes to the round-2 k_chain
+    instead of k_chain3: the 3m K = 1 BASELINE fixture through it, against the reference."""
+    path = [p for p in FULL if os.path.basename(p) == "full_3m_k1.npz"][0]
+    inp, K, expected = load_full(path)
+    monkeypatch.setenv("MZ_CHAIN_V2", "1")
+    tb = make_tb(gpu_lib, inp, K, {})
+    monkeypatch.delenv("MZ_CHAIN_V2")
+    assert tb.fused_kernel() == "k_chain<64>"
+    assert make_tb(gpu_lib, inp, K, {}).fused_kernel() == "k_chain3<64>"
+    out, _ = run_fused(tb, to_device(inp), K, {})
+    assert_same(out, expected, "gpu k_chain (MZ_CHAIN_V2) ")
 
 
 @pytest.mark.parametrize("B,A,K,S", [(256, 9, 5, 50), (128, 15, 10, 100), (64, 3, 10, 60)])
@@ -270,6 +311,45 @@ def test_device_readbacks(gpu_lib):
     torch.cuda.synchronize()
     assert np.array_equal(v.cpu().numpy(), ref["root_values"])
     assert np.array_equal(mv.cpu().numpy(), ref["marginal_visit_count"])
+
+
+def test_rebind_after_bound_stream_destroyed(gpu_lib, port_lib):
+    """mz_set_stream never queries the stream it leaves (the caller may have destroyed it): half a
+    search runs on a raw HIP stream, the stream is destroyed with that work possibly in flight, the
+    handle is rebound to torch's stream and the search finishes -- bit-exact against the port."""
+    import ctypes as C
+
+    from mazero_amd.synthetic import DEFAULTS, make_search_inputs, readbacks, run_search
+
+    B, A, K, S = 64, 9, 5, 30
+    inp = make_search_inputs(np.random.default_rng(77), B, A, S)
+    exp = run_search(make_tb(port_lib, inp, K, {}), inp, K, {}, per_sim=False)
+    hip = C.CDLL("libamdhip64.so.7")
+    raw = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(raw)) == 0
+    d = DEFAULTS
+    c2, c1, g = d["pb_c_base"], d["pb_c_init"], d["discount"]
+    dinp = to_device(inp)
+    torch.cuda.synchronize()
+    tb = make_tb(gpu_lib, inp, K, {})
+    idx = torch.empty(S, B, dtype=torch.int32, device="cuda")  # (nothing is allocated on the raw stream)
+    idy = torch.empty(B, dtype=torch.int32, device="cuda")
+    act = torch.empty(B, 1, dtype=torch.int32, device="cuda")
+    with torch.cuda.stream(torch.cuda.ExternalStream(raw.value)):
+        tb.prepare(dinp.root_reward, dinp.root_value, dinp.root_policy, dinp.root_beta, K, dinp.noise_eps,
+                   dinp.root_noise)
+        for s in range(S // 2):
+            tb.batch_selection_device(c2, c1, g, out=(idx[s], idy, act))
+            tb.batch_expansion_and_backup(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s], dinp.beta[s])
+    assert hip.hipStreamDestroy(raw) == 0
+    for s in range(S // 2, S):  # torch's current stream: the handle rebinds (mz_set_stream)
+        tb.batch_selection_device(c2, c1, g, out=(idx[s], idy, act))
+        tb.batch_expansion_and_backup(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s], dinp.beta[s])
+    torch.cuda.synchronize()
+    out = dict(sel_idx=idx.cpu().numpy())
+    out.update(readbacks(tb, g))
+    exp.pop("sel_act")
+    assert_same(out, exp, "gpu rebind ")
 
 
 def test_too_many_simulations_raise(gpu_lib):
