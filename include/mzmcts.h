@@ -119,27 +119,36 @@ int mz_create(int root_num, int agent_num, int action_space_size, int sampled_ti
 /* Replaces CTree_batch::~CTree_batch (cnode.cpp:579-587). */
 int mz_destroy(mz_batch *b);
 /* Make subsequent device work of this handle run on `stream` (a hipStream_t; NULL = default).
- * Work already queued on the previous stream is ordered before it (an event wait), unless either
- * stream is capturing a graph. */
+ * The handle's eager work already queued is ordered before it (a wait on an event each enqueueing
+ * call records behind its work), unless `stream` is capturing a graph.  The previous stream is
+ * not touched: the caller may have destroyed it. */
 int mz_set_stream(mz_batch *b, void *stream);
 /* Wait for all work of this handle and report any deferred device-side error. */
 int mz_synchronize(mz_batch *b);
 
 /* --- search ---------------------------------------------------------------------------- */
 /* Replaces CTree_batch::prepare (cnode.cpp:589-614) / Tree_batch.prepare (cytree.pyx:21-47).
- * rewards, values: [B]; policy_probs, beta, noises: [B, agent_num, A]. */
+ * rewards, values: [B]; policy_probs, beta, noises: [B, agent_num, A].
+ * Host memory (MZ_MEM_HOST): packed into the handle's pinned stage, launched, synchronised. */
 int mz_prepare(mz_batch *b, const float *rewards, const float *values, const float *policy_probs,
                const float *beta, int sampled_times, float noise_eps, const float *noises, int mem);
 
 /* Replaces CTree_batch::cbatch_selection (cnode.cpp:616-642) / Tree_batch.batch_selection
  * (cytree.pyx:50-67).  Outputs: idx_x [B] (hidden_state_index_x of the leaf's parent),
- * idy [B] (= 0..B-1), actions [B, agent_num] (action on the edge into the leaf). */
+ * idy [B] (= 0..B-1), actions [B, agent_num] (action on the edge into the leaf).
+ * Host memory: an expansion staged by mz_expand_backup(MZ_MEM_HOST) just before runs fused with
+ * this selection in one launch; the kernel writes the outputs through the stage's device mapping
+ * (MZ_HOST_COPY=1 at mz_create: one device->host copy); one synchronisation, which reports the
+ * device-side errors of both. */
 int mz_select(mz_batch *b, float pb_c_base, float pb_c_init, float discount,
               int32_t *idx_x, int32_t *idy, int32_t *actions, int mem);
 
 /* Replaces CTree_batch::cbatch_expansion_and_backup (cnode.cpp:644-670) /
  * Tree_batch.batch_expansion_and_backup (cytree.pyx:69-91).
- * rewards, values: [B]; policy_probs, beta: [B, agent_num, A]. */
+ * rewards, values: [B]; policy_probs, beta: [B, agent_num, A].
+ * Host memory: the inputs are packed into the handle's pinned stage and the launch is deferred to
+ * the handle's next call (fused with it when that is mz_select with host outputs); its device-side
+ * errors are reported by that call.  Device memory: enqueued on the handle's stream. */
 int mz_expand_backup(mz_batch *b, int hidden_state_index_x, float discount, int sampled_times,
                      const float *rewards, const float *values, const float *policy_probs,
                      const float *beta, int mem);

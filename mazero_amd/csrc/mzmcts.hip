@@ -2513,6 +2513,11 @@ __device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(
 __device__ __forceinline__ float ldsc(const float *p) {
     return *(const __attribute__((address_space(4))) float *)p;
 }
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldsc4(const float4 *p) {  // (one s_load_dwordx4)
+    const f32x4v v = *(const __attribute__((address_space(4))) f32x4v *)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 
 // std::discrete_distribution's cumulative table (libstdc++ random.tcc:2656-2690, as cdf_lane) for
 // the weights staged in sw[0 .. 64) (sw[l] = 0 for l >= A; lane l's own weight is wl): the
@@ -3686,9 +3691,21 @@ int tree_lds_bytes(int nc) {
 // scalars on every lane, the tail shift of the sorted entries lane-parallel.
 // ------------------------------------------------------------------------------------------------
 
+// The value-set scalars (C: weighted_sum, tot_weight) are read by the back-propagation for its path
+// nodes only.  Default: each back-propagation wave loads its own levels' records with scalar loads
+// (the pre-staged levels' in round 1, from the path records it already holds; later levels when it
+// reaches them), instead of a round-1 LDS-DMA of every node's record (16 bytes x the pool per tree
+// and launch, round 3).  MZ_C_STAGE builds the staged variant for A/B runs.
+#ifdef MZ_C_STAGE
+constexpr bool kTreeCStage = true;
+#else
+constexpr bool kTreeCStage = false;
+#endif
+
 struct BkPre {
     int n0, nv0, n1, nv1;  // the pre-staged levels' nodes and entry counts (nv < 0: not staged)
     int ndma;              // LDS-DMA instructions issued for them (the wave's last ones before barrier (1))
+    float4 c0, c1;         // their value-set scalars (scalar loads; unless kTreeCStage)
 };
 
 // The back-propagation's arena offsets as values of this point of the wave (they depend only on
@@ -3737,7 +3754,7 @@ template <int BK, int CAP>
 __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, int D, int k, int2 p0, int2 p1,
                                              int2 *sReg) {
     const int l = lane_id();
-    BkPre r{0, -1, 0, -1, 0};
+    BkPre r{0, -1, 0, -1, 0, make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
     const int2 *gV = d.V() + (size_t)t * P * E;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -3750,12 +3767,16 @@ __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, 
         for (int c = 0; c < 2 * pe.y; c += kWave)
             if (c + l < 2 * pe.y) glds4a(src + c + l, dst + c);
         r.ndma += (2 * pe.y + kWave - 1) / kWave;
+        // (scalar loads, counted by lgkmcnt: landed by the first LDS wait after barrier (1))
+        const float4 cw = (kTreeCStage) ? make_float4(0.f, 0.f, 0.f, 0.f) : ldsc4(d.C() + (size_t)t * P + pe.x);
         if (j == 0) {
             r.n0 = pe.x;
             r.nv0 = pe.y;
+            r.c0 = cw;
         } else {
             r.n1 = pe.x;
             r.nv1 = pe.y;
+            r.c1 = cw;
         }
     }
     return r;
@@ -3817,7 +3838,11 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         // every record of the node in one LDS round trip
         const int4 b4 = s.B[n];
         const int4 a4r = s.A[n];
-        const float4 cw = sCn[n];
+        float4 cw;
+        if (kTreeCStage) cw = sCn[n];
+        else if (j == 0 && pre.nv0 >= 0) cw = pre.c0;
+        else if (j == 1 && pre.nv1 >= 0) cw = pre.c1;
+        else cw = ldsc4(d.C() + (size_t)t * g.P + n);  // (a later level)
         const float ppn = s.PP[n];
         const float lp = s.lp[dep];
         const float key = boot[i];
@@ -3960,6 +3985,7 @@ constexpr bool kTreeCW4 = true;
 #else
 constexpr bool kTreeCW4 = kTreeLevels<NC>;
 #endif
+
 
 // The chase's common levels (wave 0, uniform control flow): while the current outcome v is a child
 // (a one-member list inside the table, tree_select_prep's next node) and the path stays under lim
@@ -4362,7 +4388,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             dma_dwords(d.PP() + nb, lds_addr(smem) + L::oPP, ne, al);
             dma_dwords(d.Q() + nb, lds_addr(smem) + L::oQ, ne, al);
             dma_dwords(d.Par() + nb, lds_addr(smem) + L::oPar, ne, al);
-        } else if (kTreeCW4<NC> && wv == 4) {  // wave 4: the value-set scalars (kTreeCW4)
+        } else if (kTreeCStage && kTreeCW4<NC> && wv == 4) {  // wave 4: the value-set scalars (kTreeCW4)
             for (int i0 = 0; i0 < ne; i0 += kWave)
                 if (i0 + l < ne)
                     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(d.C() + nb + i0 + l), "s"(lds_addr(smem) + (unsigned)(L::oCn + 16 * i0)) : "memory", "m0");
@@ -4396,7 +4422,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                     if (wv == 2) {
                         glds16a(d.A() + nb + i0 + l, sA + i0);
                         glds16a(d.Bn() + nb + i0 + l, sB + i0);
-                        glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);  // (wave 0 stages ne)
+                        if (kTreeCStage) glds16a(d.C() + nb + i0 + l, (float4 *)(smem + L::oCn) + i0);  // (wave 0 stages ne)
                     } else if (wv == 3) {
                         glds4a(d.PP() + nb + i0 + l, sPP + i0);
                         glds4a(d.Q() + nb + i0 + l, sQ + i0);
@@ -4633,7 +4659,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         glds4a(&d.hdr()[t].nxt[l < kNxt ? l : 0], sNxt);
         glds4a((const int *)st + (l < 2 * MZ_S_COUNT ? l : 0), (int *)sSt);
         // the value-set scalars of the nodes (the back-propagation waves' path nodes read them)
-        if constexpr (!kTreeCW4<NC>)
+        if constexpr (kTreeCStage && !kTreeCW4<NC>)
         for (int i0 = 0; i0 < ne; i0 += kWave)
             if (i0 + l < ne)
                 asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(d.C() + nb + i0 + l), "s"(lds_addr(smem) + (unsigned)(L::oCn + 16 * i0)) : "memory", "m0");
@@ -5264,6 +5290,11 @@ struct mz_batch {
     float *st_in = nullptr;
     int32_t *st_sel = nullptr;
     int32_t *st_err = nullptr;
+    // zero-copy (default; MZ_HOST_COPY=1 at mz_create: DMA copies instead): the kernels read the
+    // staged inputs and write the selection straight through the stage's device mapping
+    bool zc = true;
+    const float *st_in_d = nullptr;
+    int32_t *st_sel_d = nullptr, *st_err_d = nullptr;
     hipEvent_t st_ev = nullptr;  // the last copy out of st_in has been read when this fires
     bool st_busy = false;
     bool pend = false;           // a staged host-memory expansion not launched yet
@@ -5355,10 +5386,16 @@ int ensure_device(mz_batch *b) {
 
 // Poll the handle's error word (synchronises the stream).
 int ensure_stage(mz_batch *b);
+int copy_words(mz_batch *b, void *dst, const int *src, size_t n);
 int check_device_errors(mz_batch *b) {
     int rc = ensure_stage(b);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
+    if (b->zc) {  // (a one-word kernel store into the stage's device mapping: no DMA round trip)
+        rc = copy_words(b, b->st_err_d, b->dev.err(), 1);
+        if (rc) return rc;
+    } else {
+        HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
+    }
     HIP_TRY(hipStreamSynchronize(b->stream));
     b->st_busy = false;  // (every copy out of the stage has completed)
     b->dirty = b->order_live = false;  // nothing of this handle is in flight
@@ -5689,7 +5726,7 @@ int ensure_stage(mz_batch *b) {
     const size_t w_in = r64(stage_in_words(b)), w_sel = r64(stage_sel_words(b)), w_err = 16, w_rb = r64(b->rb_words);
     const size_t bytes = 4 * (w_in + w_sel + w_err + w_rb);
     void *p = stage_cache().take(-1, bytes);
-    if (!p) HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    if (!p) HIP_TRY(hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable));
     b->stage = (char *)p;
     b->stage_bytes = bytes;
     b->st_in = (float *)p;
@@ -5697,6 +5734,22 @@ int ensure_stage(mz_batch *b) {
     b->st_err = (int32_t *)p + w_in + w_sel;
     b->rb_host = (int *)p + w_in + w_sel + w_err;
     if (!b->st_ev) HIP_TRY(hipEventCreateWithFlags(&b->st_ev, hipEventDisableTiming));
+    void *pd = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&pd, p, 0));
+    b->st_in_d = (const float *)pd;
+    b->st_sel_d = (int32_t *)pd + w_in;
+    b->st_err_d = (int32_t *)pd + w_in + w_sel;
+    return MZ_OK;
+}
+
+// where a launch reads the staged inputs: the stage itself (zero-copy) or in_dev after stage_upload
+const float *stage_src(const mz_batch *b) { return b->zc ? b->st_in_d : b->in_dev; }
+
+// a launch reading the stage was enqueued: st_in may be rewritten once it has run
+int stage_consumed(mz_batch *b) {
+    if (!b->zc) return MZ_OK;
+    HIP_TRY(hipEventRecord(b->st_ev, b->stream));
+    b->st_busy = true;
     return MZ_OK;
 }
 
@@ -5711,8 +5764,9 @@ int stage_wait(mz_batch *b) {
     return MZ_OK;
 }
 
-// the first `words` of st_in -> in_dev, one copy on the handle's stream
+// the first `words` of st_in -> in_dev, one copy on the handle's stream (none when zero-copy)
 int stage_upload(mz_batch *b, size_t words) {
+    if (b->zc) return MZ_OK;
     HIP_TRY(hipMemcpyAsync(b->in_dev, b->st_in, 4 * words, hipMemcpyHostToDevice, b->stream));
     HIP_TRY(hipEventRecord(b->st_ev, b->stream));
     b->st_busy = true;
@@ -5735,13 +5789,14 @@ void stage_pack(mz_batch *b, const float *rewards, const float *values, const fl
 StepArgs staged_expand_args(mz_batch *b) {
     const size_t B = b->B, NA = (size_t)b->NA;
     StepArgs a{};
+    const float *src = stage_src(b);
     a.hsx = b->pend_hsx;
     a.discount = b->pend_disc;
     a.K = b->pend_K;
-    a.reward = b->in_dev;
-    a.value = b->in_dev + B;
-    a.policy = b->in_dev + 2 * B;
-    a.beta = b->in_dev + 2 * B + B * NA;
+    a.reward = src;
+    a.value = src + B;
+    a.policy = src + 2 * B;
+    a.beta = src + 2 * B + B * NA;
     return a;
 }
 
@@ -5751,7 +5806,9 @@ int flush_pending(mz_batch *b) {
     b->pend = false;
     int rc = stage_upload(b, 2 * (size_t)b->B * (1 + (size_t)b->NA));
     if (rc) return rc;
-    return launch_step(b, true, false, staged_expand_args(b));
+    rc = launch_step(b, true, false, staged_expand_args(b));
+    if (rc) return rc;
+    return stage_consumed(b);
 }
 
 // Packed readback computed on the device (stream-ordered, no synchronisation).
@@ -5954,6 +6011,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     // (k_tree stages one path node's value entries per slot: E <= kBkCap)
     if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE"))
         b->tree_nc = b->nc;
+    b->zc = !getenv_flag("MZ_HOST_COPY");
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
@@ -6131,7 +6189,7 @@ int mz_prepare(mz_batch *b, const float *rewards, const float *values, const flo
         stage_pack(b, rewards, values, policy, beta, noises);
         rc = stage_upload(b, stage_in_words(b));
         if (rc) return rc;
-        float *p = b->in_dev;
+        const float *p = stage_src(b);
         a.reward = p;
         a.value = p + B;
         a.policy = p + 2 * B;
@@ -6222,9 +6280,13 @@ int mz_select(mz_batch *b, float c2, float c1, float discount, int32_t *idx_x, i
     }
     a.discount = discount;
     if (mem == MZ_MEM_HOST) {
-        a.idx_x = b->sel_dev;
-        a.idy = b->sel_dev + b->B;
-        a.act = b->sel_dev + 2 * b->B;
+        rc = ensure_stage(b);
+        if (rc) return rc;
+        // zero-copy: the kernel writes the selection into the stage's device mapping
+        int32_t *o = b->zc ? b->st_sel_d : b->sel_dev;
+        a.idx_x = o;
+        a.idy = o + b->B;
+        a.act = o + 2 * b->B;
     } else {
         a.idx_x = idx_x;
         a.idy = idy;
@@ -6233,10 +6295,9 @@ int mz_select(mz_batch *b, float c2, float c1, float discount, int32_t *idx_x, i
     rc = launch_step(b, fuse, true, a);
     if (rc) return rc;
     if (mem == MZ_MEM_HOST) {  // selection + error word into the pinned stage, one synchronisation
-        rc = ensure_stage(b);
-        if (rc) return rc;
         const size_t n = stage_sel_words(b);
-        HIP_TRY(hipMemcpyAsync(b->st_sel, b->sel_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost, b->stream));
+        if (!b->zc)
+            HIP_TRY(hipMemcpyAsync(b->st_sel, b->sel_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost, b->stream));
         rc = check_device_errors(b);
         if (rc) return rc;
         std::memcpy(idx_x, b->st_sel, sizeof(int32_t) * b->B);

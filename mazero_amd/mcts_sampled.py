@@ -160,13 +160,21 @@ class _SearchLoop:
                                                C.c_void_p(self.joint.data_ptr())), "joint_action")
                 next_h, reward, value, logits = SampledMCTS._recurrent(model, leaf, self.joint)  # :150-156
             nh = next_h.reshape(B, -1)
-            if self.pool is None:
-                pdt = torch.promote_types(self.root.dtype, nh.dtype)
-                self.pool = torch.empty((S + 1, B, nh.shape[1]), dtype=pdt, device=self.dev)
-                self.leaf = torch.empty((B, nh.shape[1]), dtype=pdt, device=self.dev)
-            if s == 0:
-                self.pool[0].copy_(self.root)
-            self.pool[s + 1].copy_(nh)  # :164
+            chain = K == 1
+            if chain:
+                # K = 1: every tree is a chain, so every selection of simulation s + 1 ends at the
+                # child created by simulation s, whose parent holds hidden_state_index_x = s + 1 for
+                # every root: the reference's gather pool[s + 1][i] (mcts_sampled.py:130-134) is row i
+                # of this network output.  No pool and no gather: the output is the next leaf batch.
+                pass
+            else:
+                if self.pool is None:
+                    pdt = torch.promote_types(self.root.dtype, nh.dtype)
+                    self.pool = torch.empty((S + 1, B, nh.shape[1]), dtype=pdt, device=self.dev)
+                    self.leaf = torch.empty((B, nh.shape[1]), dtype=pdt, device=self.dev)
+                if s == 0:
+                    self.pool[0].copy_(self.root)
+                self.pool[s + 1].copy_(nh)  # :164
             logits = logits.contiguous()
             check(lib, lib.mz_policy_glue(h, C.c_void_p(logits.data_ptr()), _dtype_code(logits),
                                           logits.shape[1] * logits.shape[2], cur * A, float(tau),
@@ -176,8 +184,9 @@ class _SearchLoop:
             v32 = value.reshape(B).float()
             if s + 1 < S:
                 tb.expansion_backup_selection_device(s + 1, disc, K, r32, v32, self.probs, self.beta, c2, c1,
-                                                     out=self.sel, pool=self.pool, gather_out=self.leaf)
-                leaf = self.leaf
+                                                     out=self.sel, pool=None if chain else self.pool,
+                                                     gather_out=None if chain else self.leaf)
+                leaf = nh if chain else self.leaf
             else:
                 tb.batch_expansion_and_backup(s + 1, disc, K, r32, v32, self.probs, self.beta)
 

@@ -10,10 +10,12 @@ driver mazero_amd.mcts_sampled. It follows the reference step by step:
   (oracle/_ref/libmzref.so) or the CPU port (oracle/_build/libmzport.so), through the
   `Tree_batch` ctypes shim.
 
-Parity status: the tree calls are pinned by tests/golden (bit-exact against the reference
-ctree). The numpy glue is the reference's own numpy expressions, restated. The reference
-driver module itself is not imported here: its package imports `ray` (core/game.py:6 via
-core/config.py:9), which this image does not have.
+Parity status: pinned.  oracle/gen_driver_golden.py runs the reference driver module itself
+(imported in the build container) and records six searches (tests/golden/driver_*.npz); this
+restatement reproduces every tree call, the network's inputs, the SearchOutput and the generator
+state of each, on the CPU port and on the reference ctree (tests/test_driver.py).  The module is
+not imported here: its package imports `ray` (core/game.py:5 via core/config.py:10), which this
+image does not have, and nothing of the reference travels to the GPU box.
 """
 from __future__ import annotations
 

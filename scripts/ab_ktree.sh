@@ -3,7 +3,7 @@
 # interleaved twice: fused-launch mean (HIP events) per run.  The configurations are
 # "name:bench args;..." from the first argument, else AB_CONFIGS, else the K > 1 ones.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-O=gpurun_out/ab; mkdir -p $O
+O=gpurun_out/ab${ALT_TAG:+_$ALT_TAG}; mkdir -p $O
 ALT=${ALT:-$PWD/mazero_amd/_build/variant_old.so}
 DEF="3m_k5:--sampled-times 5;3s5z_k5:--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5;3m_k10:--sampled-times 10"
 CONFIGS=${1:-${AB_CONFIGS:-$DEF}}

@@ -5,7 +5,8 @@
 #   bench    headline bench line (bench.py, defaults)
 #   configs  bench.py --no-cpu over CONFIGS ("name:args;name:args", default: every K>1 config)
 #   dropin   bench.py --dropin at 3m K=1 and K=5
-#   ab       interleaved A/B against ALT (default: the round-3 build)
+#   ab       interleaved A/B against each ALTS build (default: the round-3 build)
+#   stamps   MZ_STAMPS=1 phase cycles, K = 1 and K = 5
 #   search   bench_search.py (full loop with a network) + a rocprofv3 kernel trace of it
 # Every GPU step has its own time limit; any failure ends the script (no later GPU step runs).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -35,11 +36,18 @@ for st in $STEPS; do
             done ;;
         dropin)
             run dropin_k1 400 python bench.py --dropin --no-cpu --steps 10
-            run dropin_k5 400 python bench.py --dropin --no-cpu --steps 10 --sampled-times 5 ;;
-        ab)  # interleaved A/B of the product against ALT (default: the round-3 build, variant_r3.so)
-            ALT=${ALT:-$PWD/mazero_amd/_build/variant_r3.so} run ab 900 bash scripts/ab_ktree.sh \
-                "${AB_CONFIGS:-3m_k1:--sampled-times 1;2s3z_k1:--map 2s3z --roots 1024;27m_k1:--map 27m_vs_30m --sims 200;3m_k5:--sampled-times 5;3m_k10:--sampled-times 10}"
-            cat gpurun_out/ab.log ;;
+            run dropin_k5 400 python bench.py --dropin --no-cpu --steps 10 --sampled-times 5
+            run dropin_split 300 python scripts/dropin_split.py
+            MZ_HOST_COPY=1 run dropin_split_copy 300 python scripts/dropin_split.py ;;
+        ab)  # interleaved A/B of the product against each build in ALTS (default: the round-3 build)
+            for alt in ${ALTS:-r3}; do
+                ALT_TAG=$alt ALT=$PWD/mazero_amd/_build/variant_$alt.so run ab_$alt 900 bash scripts/ab_ktree.sh \
+                    "${AB_CONFIGS:-3m_k1:--sampled-times 1;2s3z_k1:--map 2s3z --roots 1024;27m_k1:--map 27m_vs_30m --sims 200;3m_k5:--sampled-times 5;3m_k10:--sampled-times 10}"
+                cat gpurun_out/ab_$alt.log
+            done ;;
+        stamps)  # per-phase cycles (MZ_STAMPS=1 diagnostic build) for K = 1 and K = 5
+            MZ_STAMPS=1 run stamps_k1 300 python bench.py --no-cpu --steps 5
+            MZ_STAMPS=1 run stamps_k5 300 python bench.py --no-cpu --steps 5 --sampled-times 5 ;;
         search)
             run search 600 python bench_search.py
             MZ_TRACE_MARKS=1 run search_trace 600 rocprofv3 --kernel-trace --stats --output-format csv \

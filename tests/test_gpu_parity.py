@@ -100,15 +100,20 @@ def test_golden_host_path(gpu_lib, path):
     assert_same(run_search(tb, inp, K, knobs), expected, "gpu(host) ")
 
 
+@pytest.mark.parametrize("copy", [False, True], ids=["zero_copy", "dma_copy"])
 @pytest.mark.parametrize("path", TRACES, ids=IDS)
-def test_golden_host_path_fused(gpu_lib, path):
+def test_golden_host_path_fused(gpu_lib, path, copy, monkeypatch):
     """The host-memory path as the reference driver calls it (batch_selection, then
     batch_expansion_and_backup, no readback in between): each staged expansion is launched fused
-    with the next selection, one host->device and one device->host copy per simulation."""
+    with the next selection.  Zero-copy (default): the kernel reads the pinned stage and writes the
+    selection into it; MZ_HOST_COPY=1: one host->device and one device->host copy per simulation."""
     from mazero_amd.synthetic import run_search
 
     inp, knobs, K, expected = load_trace(path)
+    if copy:
+        monkeypatch.setenv("MZ_HOST_COPY", "1")
     tb = make_tb(gpu_lib, inp, K, knobs)
+    monkeypatch.delenv("MZ_HOST_COPY", raising=False)
     expected = {k: v for k, v in expected.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
     assert_same(run_search(tb, inp, K, knobs, per_sim=False), expected, "gpu(host, fused) ")
 
