@@ -49,6 +49,23 @@ int mz_state_changed(mz_batch *b);
 int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
                    float sampled_tau, float *probs_out, float *beta_out);
 
+/* Root preprocessing of a search (mcts_sampled.py:64-100), the arguments of prepare (:102-106):
+ *   probs  = softmax of the current agent's logits, in the logits' dtype
+ *   legal != NULL: probs *= legal, probs += legal * 1e-4, renormalised; noises likewise
+ *   beta   = probs * (1 - noise_eps) + noises * noise_eps, ** (1 / sampled_tau), *= legal,
+ *            renormalised
+ * with numpy 2.x's dtype rules: the masking arithmetic of an integer legal array in float64,
+ * stored back into the array's dtype with one rounding; a float16 array times a Python float in
+ * float16; a float16 plus a float32 array in float32.
+ * logits: [B, num_agents, A] (row stride `row_stride` elements, the agent's A logits at element
+ * `col_offset`), dtype `dtype`.  legal: the agent's legal mask as int32 [B, legal_stride] (the
+ * caller converts an integer/bool array whose values fit) or NULL.  noises: the Dirichlet draws
+ * already converted to float32 [B, A] (np_random stays on the host).  Outputs float32 [B, A].
+ * sampled_tau != 1 uses the device powf (not pinned to glibc's). */
+int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
+                 const int32_t *legal, int64_t legal_stride, const float *noises, double noise_eps,
+                 float sampled_tau, float *probs_out, float *beta_out, float *noises_out);
+
 /* Estimated joint action of one simulation (mcts_sampled.py:116-147):
  *   joint[i, k] = factor[i, k]                      for k <  current_agent  (factor int32 [B, factor_cols])
  *   joint[i, k] = actions[i]                        for k == current_agent  (selection output, int32 [B])

@@ -134,6 +134,106 @@ __global__ __launch_bounds__(kWave) void k_policy_glue(const void *logits, long 
     }
 }
 
+// float64 -> float16 with one rounding (round to nearest, ties to even), as numpy casts a float64
+// result into a float16 array (npy_double_to_half); via float32 it would round twice.
+__device__ float round_d2h(double d) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+    const unsigned short sign = (unsigned short)((b >> 48) & 0x8000u);
+    const int ex = (int)((b >> 52) & 0x7ff);
+    const unsigned long long mant = b & 0xfffffffffffffull;
+    unsigned short h;
+    if (ex == 0x7ff) {
+        h = (unsigned short)(sign | 0x7c00u | (mant ? 0x200u : 0u));  // inf / NaN
+    } else if (ex == 0) {
+        h = sign;  // double zero / subnormal: far below half's range
+    } else {
+        int e = ex - 1023 + 15;                               // half's biased exponent
+        const unsigned long long m = (1ull << 52) | mant;     // 53-bit significand
+        const int shift = (e >= 1) ? 42 : 42 + (1 - e);       // bits dropped (subnormal results: more)
+        if (shift >= 64) {
+            h = sign;
+        } else {
+            unsigned long long q = m >> shift;
+            const unsigned long long rem = m & ((1ull << shift) - 1ull), half = 1ull << (shift - 1);
+            if (rem > half || (rem == half && (q & 1ull))) ++q;
+            if (e >= 1) {
+                if (q == (1ull << 11)) {  // the rounding carried into the next binade
+                    q >>= 1;
+                    ++e;
+                }
+                h = (e >= 31) ? (unsigned short)(sign | 0x7c00u) : (unsigned short)(sign | (e << 10) | (q & 0x3ffu));
+            } else {
+                h = (unsigned short)(sign | q);  // subnormal (q == 0x400: the smallest normal)
+            }
+        }
+    }
+    return __half2float(__ushort_as_half(h));
+}
+
+// a float64 result stored into an array of the logits' dtype
+template <bool F16>
+__device__ __forceinline__ float store_d(double v) {
+    if constexpr (F16) return round_d2h(v);
+    return (float)v;
+}
+
+// Root preprocessing of mcts_sampled.py:64-100 for root blockIdx.x (prepare's policy, beta and noise
+// arguments, :102-106), with numpy 2.x's dtype rules (NEP 50):
+//   probs = softmax(logits) in the logits' dtype                                       :64-65
+//   legal (integer array): probs *= legal; probs += legal * 1e-4 (float64 arithmetic, stored in the
+//     logits' dtype); probs /= sum(probs); noises (float32) likewise                     :73-83
+//   beta = probs * (1 - eps) [logits' dtype] + noises * eps [float32] -> float32          :93
+//   beta **= 1 / tau; beta *= legal (float64, stored float32); beta /= sum(beta)          :94-100
+// `legal` holds the agent's row as int32 (the caller checked the integer array's values fit), or is
+// null.  The Dirichlet noise is drawn by the caller (np_random order) and arrives as float32.
+template <bool F16>
+__global__ __launch_bounds__(kWave) void k_root_glue(const void *logits, long long row_stride, long long col_off,
+                                                     int A, const int *legal, long long legal_stride,
+                                                     const float *noise_in, double one_minus_eps, double eps,
+                                                     int use_pow, float tau_inv, float *probs, float *beta,
+                                                     float *noise_out) {
+    __shared__ float lds[kWave];
+    __shared__ float acc[9];
+    const int t = blockIdx.x;
+    const int l = threadIdx.x;
+    const bool on = l < A;
+    const float x = on ? load_elem<F16>(logits, (long long)t * row_stride + col_off + l) : -INFINITY;
+    const bool nan_any = __ballot(on && (x != x)) != 0;
+    const float m = nan_any ? NAN : wave_max(on ? x : -INFINITY);
+    const float d = round_as<F16>(x - m);
+    const float e = round_as<F16>(np_expf(d));
+    const float s = round_as<F16>(np_row_sum(e, l, A, lds, acc));
+    float p = round_as<F16>(e / s);
+    float n = on ? noise_in[(long long)t * A + l] : 0.f;
+    double lg = 0.0;
+    if (legal) {
+        lg = on ? (double)legal[(long long)t * legal_stride + l] : 0.0;
+        const double tiny = lg * 1e-4;  // `legal * 1e-4`: a float64 array
+        p = store_d<F16>((double)p * lg);
+        p = store_d<F16>((double)p + tiny);
+        const float sp = round_as<F16>(np_row_sum(p, l, A, lds, acc));
+        p = round_as<F16>(p / sp);
+        n = (float)((double)n * lg);
+        n = (float)((double)n + tiny);
+        const float sn = np_row_sum(n, l, A, lds, acc);
+        n = n / sn;
+    }
+    // probs * (1 - eps): the Python float becomes the array's dtype (NEP 50); noises * eps in float32;
+    // the sum of a half and a float32 array is float32
+    const float c1 = store_d<F16>(one_minus_eps), c2 = (float)eps;
+    const float a1 = round_as<F16>(p * c1);
+    float b = a1 + n * c2;
+    if (use_pow) b = powf(b, tau_inv);
+    if (legal) b = (float)((double)b * lg);
+    const float sb = np_row_sum(b, l, A, lds, acc);
+    b = b / sb;
+    if (on) {
+        probs[(long long)t * A + l] = p;
+        beta[(long long)t * A + l] = b;
+        noise_out[(long long)t * A + l] = n;
+    }
+}
+
 // mcts_sampled.py:116-147 for root blockIdx.x: previous agents from `factor`, the current agent
 // from the selection, the following agents by numpy argmax of the leaf policy logits.
 template <bool F16>
@@ -181,6 +281,37 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
     else
         hipLaunchKernelGGL(k_policy_glue<false>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
                            (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out);
+    mz_internal_enqueued(b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    return MZ_OK;
+}
+
+int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
+                 const int32_t *legal, int64_t legal_stride, const float *noises, double noise_eps,
+                 float sampled_tau, float *probs_out, float *beta_out, float *noises_out) {
+    int B = 0, A = 0;
+    hipStream_t stream = nullptr;
+    int rc = mz_internal_launch_info(b, &B, &A, &stream);
+    if (rc) return rc;
+    if (!logits || !noises || !probs_out || !beta_out || !noises_out)
+        return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: null buffer");
+    if (dtype != MZ_DT_F32 && dtype != MZ_DT_F16) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: bad dtype");
+    if (row_stride < A || col_offset < 0 || col_offset + A > row_stride)
+        return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: logits row does not hold the agent's actions");
+    if (legal && legal_stride < A) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: legal rows hold fewer than A");
+    if (!(sampled_tau > 0.f)) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: sampled_tau must be > 0");
+    const float tau_inv = (float)(1.0 / (double)sampled_tau);
+    const int use_pow = (1.0 / (double)sampled_tau) != 1.0;
+    const double ome = 1.0 - noise_eps;  // (Python float arithmetic)
+    if (dtype == MZ_DT_F16)
+        hipLaunchKernelGGL(k_root_glue<true>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
+                           (long long)col_offset, A, (const int *)legal, (long long)legal_stride, noises, ome,
+                           noise_eps, use_pow, tau_inv, probs_out, beta_out, noises_out);
+    else
+        hipLaunchKernelGGL(k_root_glue<false>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
+                           (long long)col_offset, A, (const int *)legal, (long long)legal_stride, noises, ome,
+                           noise_eps, use_pow, tau_inv, probs_out, beta_out, noises_out);
     mz_internal_enqueued(b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));

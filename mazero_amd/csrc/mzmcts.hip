@@ -3951,8 +3951,11 @@ constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 // O(pool) / 4 waves).  Measured on one box, k_tree fused launch: 27m K = 5 (1010 nodes) 13.8 us by
 // levels against 14.1 us with tree_select_prep; 3m K = 5 (260 nodes) 10.4 against 11.6 us,
 // 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
+#ifndef MZ_LEVELS_FROM  // (experiment builds: the smallest class that walks by levels)
+#define MZ_LEVELS_FROM 1024
+#endif
 template <int NC>
-constexpr bool kTreeLevels = (NC >= 1024);
+constexpr bool kTreeLevels = (NC >= MZ_LEVELS_FROM);
 
 // pb_c of the prior scores from the host table in HBM (one gather per node, L2-resident) instead of
 // the staged per-n factors and a double division per node: the gather's wait leaves the SIMD to the

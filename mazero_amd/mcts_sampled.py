@@ -13,10 +13,12 @@ and the per-simulation glue stay on the device:
     model.dynamics + model.prediction       the model's own kernels, inverse transforms included
     policy softmax + beta                   mz_policy_glue (numpy float32/float16 arithmetic)
 
-so a search has no host synchronisation between `prepare` and the final readback.  Root
-preprocessing stays on the host in numpy, exactly as the reference does it
-(mcts_sampled.py:51-106): it consumes `np_random` (Dirichlet noise, then the tree seed) and runs
-once per search.
+so a search has no host synchronisation between `prepare` and the final readback.  The root
+preprocessing (mcts_sampled.py:51-106) is split: the host draws from `np_random` (the Dirichlet
+noise, then the tree seed, in the reference's order) and packs the raw root inputs into one pinned
+upload; the softmax, the legal masks and beta run on the device (mz_root_glue, numpy's dtype rules
+restated) inside the recorded loop.  Inputs the kernel does not cover (float legal masks, other
+logits dtypes) take the host path, `root_inputs`, numpy exactly as the reference computes it.
 
 Model interface (core/model.py:45-79): `prediction(h) -> (policy_logits [B,N,A], value_logits)`,
 `dynamics(h, joint_action [B,N]) -> (next_h, reward_logits)`, `inverse_value_transform`,
@@ -107,11 +109,33 @@ class _SearchLoop:
     Every input is copied into the static buffers before a run, and the tree seed lives in device
     memory (mz_reseed), so replaying the graph is a new search."""
 
-    def __init__(self, tb, B, A, N, cur, hidden, dev, model):
+    def __init__(self, tb, B, A, N, cur, hidden, dev, model, root_mode=None):
         self.tb, self.B, self.A, self.N, self.cur, self.dev = tb, B, A, N, cur, dev
         self.model_ref = weakref.ref(model)  # the captured graph reads this model's parameters
         self.root = torch.empty_like(hidden.reshape(B, -1))
         self.rin = [torch.empty(n, dtype=torch.float32, device=dev) for n in (B, B, B * A, B * A, B * A)]
+        # root_mode = (logits dtype code, has legal): the root preprocessing runs on the device
+        # (mz_root_glue) from one packed upload of the raw root inputs; None: the host computes the
+        # prepare arguments (SampledMCTS.root_inputs)
+        self.root_mode = root_mode
+        if root_mode is not None:
+            dt_code, has_legal = root_mode
+            ld = np.float16 if dt_code == MZ_DT_F16 else np.float32
+            secs = [("rewards", np.float32, B), ("values", np.float32, B), ("noise", np.float32, B * A)]
+            if has_legal:
+                secs.append(("legal", np.int32, B * A))
+            secs.append(("logits", ld, B * A))
+            off, self.sec = 0, {}
+            for name, dt, n in secs:
+                self.sec[name] = (off, dt, n)
+                off += (np.dtype(dt).itemsize * n + 15) & ~15
+            self.raw_host = torch.empty(off, dtype=torch.uint8, pin_memory=True)
+            self.raw = torch.empty(off, dtype=torch.uint8, device=dev)
+            self.raw_ev = None
+            hv = self.raw_host.numpy()
+            self.host_view = {k: hv[o:o + np.dtype(dt).itemsize * n].view(dt) for k, (o, dt, n) in self.sec.items()}
+            tdt = {np.float32: torch.float32, np.float16: torch.float16, np.int32: torch.int32}
+            self.dev_view = {k: self.raw[o:o + np.dtype(dt).itemsize * n].view(tdt[dt]) for k, (o, dt, n) in self.sec.items()}
         self.sel = (torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev),
                     torch.empty(B, 1, dtype=torch.int32, device=dev))
         self.joint = torch.empty(B, N, dtype=torch.int64, device=dev)
@@ -127,8 +151,23 @@ class _SearchLoop:
 
     def load(self, hidden, root_arrays, factor):
         self.root.copy_(hidden.reshape(self.B, -1))
-        for t, a in zip(self.rin, root_arrays):
-            t.copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+        if self.root_mode is None:
+            for t, a in zip(self.rin, root_arrays):
+                t.copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
+        else:  # the raw root inputs: packed in pinned memory, one host->device copy
+            if self.raw_ev is not None:
+                self.raw_ev.synchronize()  # (the previous search's copy has read the pinned buffer)
+            dev_logits = None
+            for k, a in root_arrays.items():
+                if isinstance(a, torch.Tensor):  # device logits: copied on the device below
+                    dev_logits = a
+                    continue
+                np.copyto(self.host_view[k], np.asarray(a).reshape(-1), casting="no")
+            self.raw.copy_(self.raw_host, non_blocking=True)
+            self.raw_ev = torch.cuda.Event()
+            self.raw_ev.record()
+            if dev_logits is not None:
+                self.dev_view["logits"].copy_(dev_logits.reshape(-1))
         if self.cur > 0:
             if isinstance(factor, torch.Tensor):  # previous agents' actions, already on the device
                 self.fac.copy_(factor[:, : self.cur])
@@ -143,6 +182,15 @@ class _SearchLoop:
         K, S = cfg.sampled_action_times, cfg.num_simulations
         r = self.rin
         model.eval()
+        if self.root_mode is not None:  # root preprocessing on the device, mcts_sampled.py:64-100
+            dv = self.dev_view
+            lg = dv.get("legal")
+            check(lib, lib.mz_root_glue(h, C.c_void_p(dv["logits"].data_ptr()), self.root_mode[0], A, 0,
+                                        None if lg is None else C.c_void_p(lg.data_ptr()), A,
+                                        C.c_void_p(dv["noise"].data_ptr()), float(eps), float(tau),
+                                        C.c_void_p(r[2].data_ptr()), C.c_void_p(r[3].data_ptr()),
+                                        C.c_void_p(r[4].data_ptr())), "root_glue")
+            r = [dv["rewards"], dv["values"], r[2], r[3], r[4]]
         # prepare + the first selection (the root's forced first child) in one launch
         tb.prepare_selection_device(r[0], r[1], r[2], r[3], K, eps, r[4], c2, c1, disc, out=self.sel)
         act = self.sel[2]
@@ -233,7 +281,7 @@ class SampledMCTS:
     """mcts_sampled.py:29-32.  `lib` selects the tree library (default: the MI355X product)."""
 
     def __init__(self, config, np_random: np.random.RandomState = None, *, lib=None, use_graph: bool = True,
-                 root_shard: Tuple[int, int, int] = None):
+                 root_shard: Tuple[int, int, int] = None, device_root: bool = True):
         """`root_shard` = (lo, hi, total): this instance searches roots [lo, hi) of a batch of `total`
         roots sharded over ranks (mazero_amd.workers).  Every rank holds the same `np_random` state;
         the per-root draws (Dirichlet noise here, select_action's uniforms in consume) are drawn for
@@ -249,6 +297,9 @@ class SampledMCTS:
             root_shard = (lo, hi, total)
         self.root_shard = root_shard
         self.use_graph = use_graph
+        # root preprocessing (softmax, masks, beta) on the device (mz_root_glue); False: in numpy on
+        # the host (root_inputs), as the reference computes it
+        self.device_root = device_root
 
     # ---------------------------------------------------------------------------------------
     def root_inputs(self, network_output, current_agent_idx, legal_actions_lst, add_noise, sampled_tau):
@@ -286,6 +337,46 @@ class SampledMCTS:
         values = _np(network_output.value).reshape(B).astype(np.float32)
         return (rewards, values, probs.astype(np.float32), beta.astype(np.float32), eps,
                 noises.astype(np.float32, copy=False)), seed
+
+    def root_raw(self, network_output, current_agent_idx, legal_actions_lst, add_noise):
+        """The raw root inputs of the device root preprocessing (mz_root_glue): the Dirichlet draws
+        (np_random, then the tree seed, in the reference's order, mcts_sampled.py:68,89) and the
+        arrays to upload, or None when the device path does not cover the inputs' dtypes (the host
+        path, root_inputs, takes them).  Returns (arrays, (logits dtype code, has legal), eps, seed)."""
+        cfg = self.config
+        A = cfg.action_space_size
+        B = network_output.hidden_state.shape[0]
+        lg = network_output.policy_logits
+        if isinstance(lg, torch.Tensor):
+            if not lg.is_cuda or lg.dtype not in (torch.float32, torch.float16):
+                return None
+            logits = lg[:, current_agent_idx, :]
+            code = _dtype_code(lg)
+        else:
+            lg = np.asarray(lg)
+            if lg.dtype not in (np.float32, np.float16):
+                return None
+            logits = lg[:, current_agent_idx, :]
+            code = MZ_DT_F16 if lg.dtype == np.float16 else MZ_DT_F32
+        legal = None
+        if legal_actions_lst is not None:
+            la = _np(legal_actions_lst)
+            if la.dtype.kind not in "iub":
+                return None  # (float masks: numpy's float arithmetic differs; the host path)
+            legal = la[:, current_agent_idx, :]
+            if legal.dtype.kind != "b" and legal.size and (legal.min() < -(1 << 31) or legal.max() >= (1 << 31)):
+                return None
+            legal = legal.astype(np.int32)
+        alpha, eps = cfg.root_dirichlet_alpha, cfg.root_exploration_fraction
+        noise = self.draw_rows(lambda n: self.np_random.dirichlet([alpha] * A, n), B).astype(np.float32)
+        if not add_noise:
+            eps = 0.0
+        seed = self.np_random.choice(256)  # drawn after the noise, :89
+        arrays = dict(rewards=_np(network_output.reward).reshape(B).astype(np.float32),
+                      values=_np(network_output.value).reshape(B).astype(np.float32), noise=noise, logits=logits)
+        if legal is not None:
+            arrays["legal"] = legal
+        return arrays, (code, legal is not None), eps, seed
 
     def draw_rows(self, draw, B: int) -> np.ndarray:
         """`draw(n)` -> n per-root rows from np_random; with a root shard the whole batch's rows are
@@ -348,13 +439,18 @@ class SampledMCTS:
         dev = hidden.device
         B = hidden.shape[0]
 
-        (rr, rv, rp, rb, eps, rn), seed = self.root_inputs(network_output, cur, legal_actions_lst, add_noise,
-                                                           sampled_tau)
+        raw = self.root_raw(network_output, cur, legal_actions_lst, add_noise) if self.device_root else None
+        if raw is not None:
+            root_arrays, root_mode, eps, seed = raw
+        else:
+            (rr, rv, rp, rb, eps, rn), seed = self.root_inputs(network_output, cur, legal_actions_lst, add_noise,
+                                                               sampled_tau)
+            root_arrays, root_mode = (rr, rv, rp, rb, rn), None
         with torch.cuda.device(dev):
             tb = self._tree(B, seed, dev)
             # the discount is a kernel argument of the recorded launches
             key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), float(disc), tuple(hidden.shape),
-                   hidden.dtype)
+                   hidden.dtype, root_mode)
             for k in [k for k, v in _LOOPS.items() if v.model_ref() is None]:
                 del _LOOPS[k]  # loops (graph, pool) of models that no longer exist
             st = _LOOPS.get(key)
@@ -362,9 +458,9 @@ class SampledMCTS:
             # ids are reused once an object is freed; a recorded graph reads the parameters at the
             # addresses it was recorded with (re-homed weights, weights.FlatWeights, need a new one)
             if st is None or st.model_ref() is not model or st.storage != sig:
-                st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model)
+                st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model, root_mode)
                 st.storage = sig
-            st.load(hidden, (rr, rv, rp, rb, rn), factor)
+            st.load(hidden, root_arrays, factor)
             with torch.no_grad():
                 if self.use_graph and st.runs > 0 and st.graph is None:
                     st.capture(model, cfg, eps, sampled_tau)  # (records only: nothing runs)

@@ -7,6 +7,7 @@
 #   dropin   bench.py --dropin at 3m K=1 and K=5
 #   ab       interleaved A/B against each ALTS build (default: the round-3 build)
 #   stamps   MZ_STAMPS=1 phase cycles, K = 1 and K = 5
+#   micro    scripts/_gridsize: launch period against grid and workgroup size
 #   search   bench_search.py (full loop with a network) + a rocprofv3 kernel trace of it
 # Every GPU step has its own time limit; any failure ends the script (no later GPU step runs).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
@@ -48,6 +49,8 @@ for st in $STEPS; do
         stamps)  # per-phase cycles (MZ_STAMPS=1 diagnostic build) for K = 1 and K = 5
             MZ_STAMPS=1 run stamps_k1 300 python bench.py --no-cpu --steps 5
             MZ_STAMPS=1 run stamps_k5 300 python bench.py --no-cpu --steps 5 --sampled-times 5 ;;
+        micro)  # launch period against grid / workgroup size (scripts/gridsize.hip, built beforehand)
+            run gridsize 120 ./scripts/_gridsize ;;
         search)
             run search 600 python bench_search.py
             MZ_TRACE_MARKS=1 run search_trace 600 rocprofv3 --kernel-trace --stats --output-format csv \

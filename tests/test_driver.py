@@ -570,8 +570,9 @@ def test_oracle_driver_matches_reference_driver(path, tree, request):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("device_root", [True, False], ids=["device_root", "host_root"])
 @pytest.mark.parametrize("path", _DRIVER_FX, ids=_fx_id)
-def test_device_driver_matches_reference_driver(path):
+def test_device_driver_matches_reference_driver(path, device_root):
     """mazero_amd.mcts_sampled.SampledMCTS, fed the reference network's recorded outputs,
     reproduces the reference driver's search bit for bit: the leaf rows it gathers and the joint
     actions it builds (the network's inputs), every SearchOutput field and the np_random state
@@ -587,13 +588,13 @@ def test_device_driver_matches_reference_driver(path):
     for run in range(3):  # eager, capture + replay, replay
         net.reset()
         rng = fx.np_random()
-        got = SampledMCTS(fx.config(), rng).batch_search(net, root, fx.agent, fx.factor, fx.N, fx.legal, device=dev,
-                                                         add_noise=fx.meta["add_noise"])
+        got = SampledMCTS(fx.config(), rng, device_root=device_root).batch_search(
+            net, root, fx.agent, fx.factor, fx.N, fx.legal, device=dev, add_noise=fx.meta["add_noise"])
         torch.cuda.synchronize()
         net.check_inputs()
         _compare_outputs(got, fx.expected())
         np.testing.assert_array_equal(np.asarray(rng.random(4)), fx.z["rng_after"])
-    loop = [v for v in _LOOPS.values() if v.model_ref() is net][0]
+    loop = [v for v in _LOOPS.values() if v.model_ref() is net and (v.root_mode is not None) == device_root][0]
     assert isinstance(loop.graph, torch.cuda.CUDAGraph), "the third search did not replay a graph"
 
 
@@ -624,3 +625,116 @@ def test_graph_census_counts_child_graph_memsets():
     assert (total.value, memsets.value) == (2, 1)
     hip.hipGraphDestroy(parent)
     hip.hipGraphDestroy(child)
+
+
+# ------------------------------------------------------------------------------------------------
+# Device root preprocessing (mz_root_glue)
+# ------------------------------------------------------------------------------------------------
+def _round_d2h_restated(d: np.ndarray) -> np.ndarray:
+    """mzdriver.hip round_d2h, line by line on uint64 bit patterns: float64 -> float16 with one
+    rounding (ties to even).  Returns the float16 bit patterns."""
+    b = np.asarray(d, np.float64).view(np.uint64)
+    out = np.empty(b.shape, np.uint16)
+    for i, v in enumerate(b.reshape(-1).tolist()):
+        sign = (v >> 48) & 0x8000
+        ex = (v >> 52) & 0x7FF
+        mant = v & 0xFFFFFFFFFFFFF
+        if ex == 0x7FF:
+            h = sign | 0x7C00 | (0x200 if mant else 0)
+        elif ex == 0:
+            h = sign
+        else:
+            e = ex - 1023 + 15
+            m = (1 << 52) | mant
+            shift = 42 if e >= 1 else 42 + (1 - e)
+            if shift >= 64:
+                h = sign
+            else:
+                q = m >> shift
+                rem, half = m & ((1 << shift) - 1), 1 << (shift - 1)
+                if rem > half or (rem == half and (q & 1)):
+                    q += 1
+                if e >= 1:
+                    if q == (1 << 11):
+                        q >>= 1
+                        e += 1
+                    h = (sign | 0x7C00) if e >= 31 else (sign | (e << 10) | (q & 0x3FF))
+                else:
+                    h = sign | q
+        out.reshape(-1)[i] = h
+    return out
+
+
+def test_double_to_half_rounding_restatement():
+    """The kernel's float64 -> float16 rounding equals numpy's astype(float16) (one rounding), on
+    random values over half's whole range, its subnormals, the overflow boundary and exact ties."""
+    rng = np.random.default_rng(0)
+    xs = [
+        rng.standard_normal(20000) * 10.0 ** rng.integers(-9, 6, 20000),
+        rng.random(5000) * 2.0 ** -14,                     # half subnormals
+        65504.0 + rng.random(3000) * 40.0,                  # overflow boundary (65520 rounds to inf)
+        (np.arange(-2048, 2048) + 0.5) * 2.0 ** -10,        # ties at many binades
+        (np.arange(1, 2000) + 0.5) * 2.0 ** -24,            # subnormal ties
+        np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-300, -1e-300, 2.0 ** -25, 3 * 2.0 ** -26, 1e-4, 6e-5]),
+    ]
+    for x in xs:
+        x = x.astype(np.float64)
+        got = _round_d2h_restated(x)
+        exp = x.astype(np.float16).view(np.uint16)
+        nan = np.isnan(x)
+        np.testing.assert_array_equal(got[~nan], exp[~nan])
+        assert np.all((got[nan] & 0x7C00) == 0x7C00) and np.all(got[nan] & 0x3FF)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+@pytest.mark.parametrize("A", [3, 9, 15, 36, 64])
+def test_root_glue_matches_host_root_inputs(dtype, A):
+    """mz_root_glue against the host root preprocessing (SampledMCTS.root_inputs, the reference's
+    numpy expressions, pinned to the reference driver by the driver_*.npz fixtures), bit for bit:
+    legal masks as int64 and bool with zeros, none; noise on and off; extreme logits."""
+    import torch
+
+    from mazero_amd._capi import MZ_DT_F16, MZ_DT_F32, check
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import NetworkOutput, SearchConfig
+
+    B, N, cur = 300, 3, 1
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(A)
+    tb = _handle(B, A)
+    cfg = SearchConfig(action_space_size=A)
+    for legal_kind in ("none", "int64", "bool"):
+        for noise in (True, False):
+            logits = (rng.standard_normal((B, N, A)) * rng.choice([0.1, 1, 4, 30], size=(B, 1, 1))).astype(dtype)
+            logits[:5, cur, 1 % A] = 60.0  # one dominant logit
+            legal = None
+            if legal_kind != "none":
+                legal = (rng.random((B, N, A)) >= 0.3).astype(np.int64)
+                legal[..., 0] = np.where(legal.sum(-1) == 0, 1, legal[..., 0])
+                if legal_kind == "bool":
+                    legal = legal.astype(bool)
+            out = NetworkOutput(torch.zeros(B, 4, device=dev), rng.standard_normal((B, 1)).astype(np.float32),
+                                rng.standard_normal((B, 1)).astype(np.float32), logits)
+            seed = int(rng.integers(1 << 30))
+            m_host, m_dev = SampledMCTS(cfg, np.random.RandomState(seed)), SampledMCTS(cfg, np.random.RandomState(seed))
+            (rr, rv, rp, rb, eps, rn), seed_h = m_host.root_inputs(out, cur, legal, noise, 1.0)
+            arrays, mode, eps_d, seed_d = m_dev.root_raw(out, cur, legal, noise)
+            assert seed_d == seed_h and eps_d == eps and mode == (MZ_DT_F16 if dtype == "float16" else MZ_DT_F32,
+                                                                  legal is not None)
+            t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in arrays.items()}
+            probs, beta, nz = (torch.empty(B, A, device=dev) for _ in range(3))
+            tb._sync_stream()
+            lg = t.get("legal")
+            rc = tb._lib.mz_root_glue(tb._h, C.c_void_p(t["logits"].data_ptr()), mode[0], A, 0,
+                                      None if lg is None else C.c_void_p(lg.data_ptr()), A,
+                                      C.c_void_p(t["noise"].data_ptr()), float(eps_d), 1.0,
+                                      C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr()),
+                                      C.c_void_p(nz.data_ptr()))
+            check(tb._lib, rc, "root_glue")
+            where = f"{dtype} A={A} legal={legal_kind} noise={noise}"
+            for got, exp, name in ((probs, rp, "probs"), (beta, rb, "beta"), (nz, rn, "noises")):
+                np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), exp.reshape(B, A).view(np.uint32),
+                                              err_msg=f"{name} {where}")
+            np.testing.assert_array_equal(arrays["rewards"], rr)
+            np.testing.assert_array_equal(arrays["values"], rv)
