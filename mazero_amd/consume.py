@@ -126,6 +126,28 @@ class SelfPlayDecisions(NamedTuple):
     outputs: List[DeviceSearchOutput]
 
 
+def torch_eps_uniforms(legal_rows) -> Tuple[np.ndarray, np.ndarray]:
+    """The epsilon-greedy draws of eps_greedy_action (core/utils.py:319-334) from torch's global CPU
+    generator, exactly as the reference's worker loop makes them: root after root, one
+    `torch.rand_like` (float32) then one `Categorical(mask).sample()`.  Returned as the uniforms the
+    device kernel (mz_eps_greedy) takes: u_eps is the float32 draw itself; u_cat is the lower edge of
+    the sampled action's interval of the mask's cumulative weights, c[a-1] / total in float64, which
+    the kernel's inverse cdf maps back to exactly that action (a positive-weight action: the sample's
+    own).  legal_rows: [B, A] (the agent's rows, the reference's array dtype).  A host loop over the
+    roots, as the reference's: for replaying the reference's torch stream bit for bit."""
+    rows = np.asarray(legal_rows)
+    B = rows.shape[0]
+    u_eps = np.empty(B, np.float32)
+    u_cat = np.empty(B, np.float64)
+    for i in range(B):
+        mask = torch.from_numpy(np.ascontiguousarray(rows[i]))
+        u_eps[i] = float(torch.rand_like(mask[..., 0].float()))
+        a = int(torch.distributions.Categorical(mask).sample())
+        c = np.cumsum(rows[i].astype(np.int64))
+        u_cat[i] = 0.0 if a == 0 else float(c[a - 1]) / float(c[-1])
+    return u_eps, u_cat
+
+
 def selfplay_decisions(mcts, model, network_output, true_num_agents: int, legal_actions_lst, *,
                        temperature: float, sampled_tau: float = 1.0, greedy_epsilon: float = 0.0,
                        eps_uniforms: Optional[Tuple] = None, device=None) -> SelfPlayDecisions:
@@ -135,14 +157,25 @@ def selfplay_decisions(mcts, model, network_output, true_num_agents: int, legal_
 
     `mcts.np_random` is consumed exactly as the reference consumes `self.np_random`.
     eps_uniforms: optional (u_eps float32 [N, B], u_cat float64 [N, B]); drawn with torch.rand on
-    the device when omitted."""
+    the device when omitted (same distribution, not the reference's stream); "torch": drawn per agent
+    from torch's global CPU generator as the reference draws them (torch_eps_uniforms), so the
+    actions replay the reference's bit for bit (a host loop over the roots)."""
     N = int(true_num_agents)
     hidden = network_output.hidden_state
     dev = hidden.device
     B = hidden.shape[0]
     legal = _dev_i32(legal_actions_lst, dev) if legal_actions_lst is not None else \
         torch.ones(B, N, mcts.config.action_space_size, dtype=torch.int32, device=dev)
-    if eps_uniforms is None:
+    torch_stream = isinstance(eps_uniforms, str)
+    if torch_stream:
+        if eps_uniforms != "torch":
+            raise ValueError(f"eps_uniforms: {eps_uniforms!r} (a tuple of arrays or 'torch')")
+        legal_host = np.ones((B, N, mcts.config.action_space_size), np.int64) if legal_actions_lst is None \
+            else (legal_actions_lst.cpu().numpy() if isinstance(legal_actions_lst, torch.Tensor)
+                  else np.asarray(legal_actions_lst))
+        u_eps = torch.empty(N, B, dtype=torch.float32, device=dev)
+        u_cat = torch.empty(N, B, dtype=torch.float64, device=dev)
+    elif eps_uniforms is None:
         u_eps = torch.rand(N, B, dtype=torch.float32, device=dev)
         u_cat = torch.rand(N, B, dtype=torch.float64, device=dev)
     else:
@@ -158,6 +191,10 @@ def selfplay_decisions(mcts, model, network_output, true_num_agents: int, legal_
         outs.append(out)
         # select_action's np_random.choice: one double per root, in root order (:240-247)
         u = torch.from_numpy(_root_uniforms(mcts, B)).to(dev)
+        if torch_stream:  # the agent's torch draws, root by root (:250-254)
+            ue, uc = torch_eps_uniforms(legal_host[:, k, :])
+            u_eps[k].copy_(torch.from_numpy(ue))
+            u_cat[k].copy_(torch.from_numpy(uc))
         with torch.cuda.device(dev):
             _, act, ent = select_actions(out, u, temperature, deterministic=False)
             eps_greedy(out, act, legal[:, k, :], greedy_epsilon, u_eps[k], u_cat[k])  # :250-254

@@ -11,9 +11,10 @@ output -- the checker of mazero_amd.consume and include/mzconsume.h.  Only tests
                        inference
 
 Parity status: the np_random consumption is pinned against numpy's own Generator / RandomState
-`choice` (tests/test_consume.py); the epsilon-greedy comparison against torch is pinned for the
-float32 threshold and distributionally for the categorical draw (torch's CPU multinomial stream
-is not restated).
+`choice` (tests/test_consume.py).  The epsilon-greedy decision is pinned to the reference itself:
+tests/golden/eps_greedy_torch.npz holds core/utils.py's eps_greedy_action run root after root under
+a seeded torch generator (oracle/gen_driver_golden.py), and mazero_amd.consume.torch_eps_uniforms
++ eps_greedy_given (and the device kernel) reproduce those actions.
 """
 from __future__ import annotations
 

@@ -32,6 +32,9 @@ Recorded per case (see `record_case`):
   SearchOutput       every field (per-root lists padded to the widest root, with degrees)
   np_random after    the next 4 doubles the generator draws after the search
 
+and tests/golden/eps_greedy_torch.npz: core/utils.py's eps_greedy_action itself over 400 roots
+under a seeded torch generator (record_eps_greedy).
+
 Usage:  make -C oracle && python oracle/gen_driver_golden.py
 """
 from __future__ import annotations
@@ -233,6 +236,28 @@ def record_case(mcts_sampled, tree_lib_log, name, spec):
     return z
 
 
+def record_eps_greedy():
+    """core/utils.py:319-334 `eps_greedy_action` itself, root after root under a seeded torch
+    global generator (as the self-play worker calls it, selfplay_worker.py:250-254), over random
+    legal masks with zeros (int64, the reference's array dtype), for eps in {0.1, 0.5, 1.0}."""
+    from core.utils import eps_greedy_action
+
+    g = np.random.default_rng(7)
+    R, A = 400, 11
+    masks = (g.random((R, A)) >= 0.4).astype(np.int64)
+    masks[:, 0] = np.where(masks.sum(-1) == 0, 1, masks[:, 0])
+    greedy = g.integers(0, A, size=R).astype(np.int32)
+    out = {}
+    for j, eps in enumerate((0.1, 0.5, 1.0)):
+        torch.manual_seed(100 + j)
+        acts = np.array([int(eps_greedy_action(greedy[i], masks[i], eps)[0]) for i in range(R)], np.int64)
+        out[f"actions_eps{j}"] = acts
+    path = os.path.join(GOLDEN, "eps_greedy_torch.npz")
+    np.savez_compressed(path, masks=masks, greedy=greedy, eps=np.array([0.1, 0.5, 1.0]),
+                        seeds=np.array([100, 101, 102]), **out)
+    print(f"{path}: {os.path.getsize(path)} B")
+
+
 def main():
     if not os.path.exists(REF_LIB):
         sys.exit("oracle/_ref/libmzref.so missing: run `make -C oracle` first")
@@ -245,6 +270,7 @@ def main():
         path = os.path.join(GOLDEN, f"driver_{name}.npz")
         np.savez_compressed(path, **z)
         print(f"{path}: {os.path.getsize(path)} B")
+    record_eps_greedy()
 
 
 if __name__ == "__main__":

@@ -143,6 +143,47 @@ def _synthetic_output(B, A, width, rng, dev, N=1):
     return out, deg, visits, actions, marg
 
 
+def _eps_fixture():
+    import os
+
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "eps_greedy_torch.npz"))
+
+
+def test_torch_eps_draws_replay_reference_eps_greedy():
+    """mazero_amd.consume.torch_eps_uniforms turns torch's CPU stream into the kernel's uniforms:
+    with the same torch seed, eps_greedy_given (the kernel's arithmetic) reproduces the actions
+    core/utils.py's eps_greedy_action itself produced root after root (tests/golden/
+    eps_greedy_torch.npz, recorded by oracle/gen_driver_golden.py), for eps 0.1, 0.5, 1.0."""
+    from mazero_amd.consume import torch_eps_uniforms
+
+    z = _eps_fixture()
+    masks, greedy = z["masks"], z["greedy"]
+    for j, (eps, seed) in enumerate(zip(z["eps"], z["seeds"])):
+        torch.manual_seed(int(seed))
+        u_eps, u_cat = torch_eps_uniforms(masks)
+        got = [eps_greedy_given(greedy[i], masks[i], float(eps), u_eps[i], u_cat[i]) for i in range(len(greedy))]
+        np.testing.assert_array_equal(np.asarray(got, np.int64), z[f"actions_eps{j}"], err_msg=f"eps={eps}")
+
+
+@pytest.mark.gpu
+def test_eps_greedy_kernel_torch_stream():
+    """The device kernel fed torch_eps_uniforms reproduces the reference's eps_greedy_action."""
+    from mazero_amd.consume import eps_greedy, torch_eps_uniforms
+
+    dev = torch.device("cuda", 0)
+    z = _eps_fixture()
+    masks, greedy = z["masks"], z["greedy"]
+    B, A = masks.shape
+    out, *_ = _synthetic_output(B, A, 4, np.random.default_rng(3), dev)
+    legal_d = torch.from_numpy(masks.astype(np.int32)).to(dev)
+    for j, (eps, seed) in enumerate(zip(z["eps"], z["seeds"])):
+        torch.manual_seed(int(seed))
+        u_eps, u_cat = torch_eps_uniforms(masks)
+        act = torch.from_numpy(greedy.copy()).to(dev)
+        eps_greedy(out, act, legal_d, float(eps), torch.from_numpy(u_eps).to(dev), torch.from_numpy(u_cat).to(dev))
+        np.testing.assert_array_equal(act.cpu().numpy().astype(np.int64), z[f"actions_eps{j}"], err_msg=f"eps={eps}")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("temperature", [1.0, 0.5, 0.25, 0.3])
 @pytest.mark.parametrize("deterministic", [False, True])
