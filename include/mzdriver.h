@@ -49,6 +49,14 @@ int mz_state_changed(mz_batch *b);
 int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
                    float sampled_tau, float *probs_out, float *beta_out);
 
+/* numpy's np.exp of every float16 bit pattern, table[bits] = bits of np.exp(half(bits)), for the
+ * float16 paths of mz_policy_glue and mz_root_glue on the current device.  np.exp of a float16 array
+ * is evaluated by a SIMD half loop on AVX512_SKX hosts whose result differs from the float32
+ * exponential rounded to half for a few inputs; the host's numpy computes the table once
+ * (mazero_amd.mcts_sampled.ensure_half_exp).  Without a table the float16 paths round numpy's
+ * float32 SIMD exp.  Copied synchronously; call it outside a graph capture. */
+int mz_set_half_exp_table(const uint16_t *table);
+
 /* Root preprocessing of a search (mcts_sampled.py:64-100), the arguments of prepare (:102-106):
  *   probs  = softmax of the current agent's logits, in the logits' dtype
  *   legal != NULL: probs *= legal, probs += legal * 1e-4, renormalised; noises likewise

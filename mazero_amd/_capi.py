@@ -113,6 +113,7 @@ DRIVER_SIGNATURES = {
     "mz_joint_action": (_i, [_p, _p, _i, _i, _i, _p, _i, _p, _p]),
     "mz_graph_census": (_i, [_p, C.POINTER(_i), C.POINTER(_i)]),
     "mz_fused_kernel": (_i, [_p, C.c_char_p, _i]),
+    "mz_set_half_exp_table": (_i, [_p]),
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 
 #include "../../include/mzdriver.h"
 #include "mz_internal.h"
@@ -60,6 +61,22 @@ __device__ float np_expf(float x) {
 }
 
 __device__ __forceinline__ float to_half_and_back(float v) { return __half2float(__float2half_rn(v)); }
+
+// np.exp of a float16 array.  numpy does not always evaluate it as float32 exp rounded to half: on
+// AVX512_SKX hosts its half loop uses a vectorised float32 exponential of its own, which rounds to a
+// different half for a few inputs (4 of the 63,488 finite halves on this image's numpy 2.2).  The
+// host hands its numpy's answer for every half bit pattern (mz_set_half_exp_table); without that
+// table the kernels round numpy's float32 SIMD exp to half.
+__device__ __forceinline__ float np_exp_half(float d, const unsigned short *table) {
+    if (table) return __half2float(__ushort_as_half(table[__half_as_ushort(__float2half_rn(d))]));
+    return to_half_and_back(np_expf(d));
+}
+
+template <bool F16>
+__device__ __forceinline__ float np_exp_as(float d, const unsigned short *table) {
+    if constexpr (F16) return np_exp_half(d, table);
+    return np_expf(d);
+}
 
 template <bool F16>
 __device__ __forceinline__ float round_as(float v) {
@@ -110,7 +127,7 @@ __device__ __forceinline__ float wave_max(float v) {
 template <bool F16>
 __global__ __launch_bounds__(kWave) void k_policy_glue(const void *logits, long long row_stride, long long col_off,
                                                        int A, int use_pow, float tau_inv, float *probs,
-                                                       float *beta) {
+                                                       float *beta, const unsigned short *hexp) {
     __shared__ float lds[kWave];
     __shared__ float acc[9];
     const int t = blockIdx.x;
@@ -121,7 +138,7 @@ __global__ __launch_bounds__(kWave) void k_policy_glue(const void *logits, long 
     const bool nan_any = __ballot(on && (x != x)) != 0;
     const float m = nan_any ? NAN : wave_max(on ? x : -INFINITY);
     const float d = round_as<F16>(x - m);
-    const float e = round_as<F16>(np_expf(d));
+    const float e = np_exp_as<F16>(d, hexp);
     const float s = round_as<F16>(np_row_sum(e, l, A, lds, acc));
     const float p = round_as<F16>(e / s);
     // `** (1 / sampled_tau)`: numpy returns the array itself for an exponent of 1.0
@@ -191,7 +208,7 @@ __global__ __launch_bounds__(kWave) void k_root_glue(const void *logits, long lo
                                                      int A, const int *legal, long long legal_stride,
                                                      const float *noise_in, double one_minus_eps, double eps,
                                                      int use_pow, float tau_inv, float *probs, float *beta,
-                                                     float *noise_out) {
+                                                     float *noise_out, const unsigned short *hexp) {
     __shared__ float lds[kWave];
     __shared__ float acc[9];
     const int t = blockIdx.x;
@@ -201,7 +218,7 @@ __global__ __launch_bounds__(kWave) void k_root_glue(const void *logits, long lo
     const bool nan_any = __ballot(on && (x != x)) != 0;
     const float m = nan_any ? NAN : wave_max(on ? x : -INFINITY);
     const float d = round_as<F16>(x - m);
-    const float e = round_as<F16>(np_expf(d));
+    const float e = np_exp_as<F16>(d, hexp);
     const float s = round_as<F16>(np_row_sum(e, l, A, lds, acc));
     float p = round_as<F16>(e / s);
     float n = on ? noise_in[(long long)t * A + l] : 0.f;
@@ -258,9 +275,41 @@ __global__ __launch_bounds__(kWave) void k_joint_action(const void *pred, int N,
     }
 }
 
+// the table of mz_set_half_exp_table per device (allocated once, never freed: captured graphs keep
+// its address)
+constexpr int kMaxDevices = 64;
+unsigned short *g_half_exp[kMaxDevices];
+std::mutex g_half_exp_mu;
+
+// the current device's table (the launchers call this after making the handle's device current)
+const unsigned short *half_exp_table() {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_half_exp_mu);
+    return g_half_exp[dev];
+}
+
 }  // namespace
 
 extern "C" {
+
+int mz_set_half_exp_table(const uint16_t *table) {
+    if (!table) return mz_internal_fail(MZ_ERR_ARG, "mz_set_half_exp_table: null table");
+    int dev = -1;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    if (dev < 0 || dev >= kMaxDevices) return mz_internal_fail(MZ_ERR_UNSUPPORTED, "mz_set_half_exp_table: device id");
+    std::lock_guard<std::mutex> lk(g_half_exp_mu);
+    if (!g_half_exp[dev]) {
+        void *p = nullptr;
+        e = hipMalloc(&p, 65536 * sizeof(uint16_t));
+        if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+        g_half_exp[dev] = (unsigned short *)p;
+    }
+    e = hipMemcpy(g_half_exp[dev], table, 65536 * sizeof(uint16_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
+    return MZ_OK;
+}
 
 int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
                    float sampled_tau, float *probs_out, float *beta_out) {
@@ -277,10 +326,10 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
     const int use_pow = (1.0 / (double)sampled_tau) != 1.0;
     if (dtype == MZ_DT_F16)
         hipLaunchKernelGGL(k_policy_glue<true>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
-                           (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out);
+                           (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out, half_exp_table());
     else
         hipLaunchKernelGGL(k_policy_glue<false>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
-                           (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out);
+                           (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out, half_exp_table());
     mz_internal_enqueued(b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));
@@ -307,11 +356,11 @@ int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride,
     if (dtype == MZ_DT_F16)
         hipLaunchKernelGGL(k_root_glue<true>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
                            (long long)col_offset, A, (const int *)legal, (long long)legal_stride, noises, ome,
-                           noise_eps, use_pow, tau_inv, probs_out, beta_out, noises_out);
+                           noise_eps, use_pow, tau_inv, probs_out, beta_out, noises_out, half_exp_table());
     else
         hipLaunchKernelGGL(k_root_glue<false>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
                            (long long)col_offset, A, (const int *)legal, (long long)legal_stride, noises, ome,
-                           noise_eps, use_pow, tau_inv, probs_out, beta_out, noises_out);
+                           noise_eps, use_pow, tau_inv, probs_out, beta_out, noises_out, half_exp_table());
     mz_internal_enqueued(b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return mz_internal_fail(MZ_ERR_DEVICE, hipGetErrorString(e));

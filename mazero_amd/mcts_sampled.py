@@ -111,6 +111,7 @@ class _SearchLoop:
 
     def __init__(self, tb, B, A, N, cur, hidden, dev, model, root_mode=None):
         self.tb, self.B, self.A, self.N, self.cur, self.dev = tb, B, A, N, cur, dev
+        ensure_half_exp(tb._lib, dev.index if dev.index is not None else torch.cuda.current_device())
         self.model_ref = weakref.ref(model)  # the captured graph reads this model's parameters
         self.root = torch.empty_like(hidden.reshape(B, -1))
         self.rin = [torch.empty(n, dtype=torch.float32, device=dev) for n in (B, B, B * A, B * A, B * A)]
@@ -182,6 +183,10 @@ class _SearchLoop:
         K, S = cfg.sampled_action_times, cfg.num_simulations
         r = self.rin
         model.eval()
+        # bind the handle to the current stream first: the direct mz_* launches below (root glue,
+        # joint action, policy glue) run on the handle's stream, which under a capture must be the
+        # capturing one, or the launch runs at record time and is missing from the graph
+        tb._sync_stream()
         if self.root_mode is not None:  # root preprocessing on the device, mcts_sampled.py:64-100
             dv = self.dev_view
             lg = dv.get("legal")
@@ -264,6 +269,26 @@ class _SearchLoop:
 
 
 _LOOPS: dict = {}
+_HALF_EXP: set = set()  # (library, device index) pairs holding the host's float16 exp table
+
+
+def half_exp_table() -> np.ndarray:
+    """np.exp of every float16 bit pattern as this host's numpy evaluates it (uint16 bits).  numpy's
+    float16 exp is not always float32 exp rounded to half (its AVX512_SKX half loop differs in a
+    few inputs), and the reference computes the root / leaf softmax with it under autocast."""
+    with np.errstate(all="ignore"):
+        return np.exp(np.arange(1 << 16, dtype=np.uint16).view(np.float16)).view(np.uint16).copy()
+
+
+def ensure_half_exp(lib, device_index: int) -> None:
+    """Give `lib`'s float16 glue kernels on device `device_index` the host's exp table (once)."""
+    key = (id(lib), int(device_index))
+    if key in _HALF_EXP or not hasattr(lib, "mz_set_half_exp_table"):
+        return
+    t = half_exp_table()
+    with torch.cuda.device(int(device_index)):
+        check(lib, lib.mz_set_half_exp_table(t.ctypes.data_as(C.c_void_p)), "set_half_exp_table")
+    _HALF_EXP.add(key)
 
 
 def _storage_signature(model) -> tuple:

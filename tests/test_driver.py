@@ -149,9 +149,27 @@ def test_oracle_driver_runs_on_cpu(port_lib):
 # GPU
 # ------------------------------------------------------------------------------------------------
 def _handle(B, A):
-    from mazero_amd.cytree import Tree_batch
+    import torch
 
-    return Tree_batch(B, 1, A, 1, 4, 0.01, 0, 0.75, 0.8)
+    from mazero_amd.cytree import Tree_batch
+    from mazero_amd.mcts_sampled import ensure_half_exp
+
+    tb = Tree_batch(B, 1, A, 1, 4, 0.01, 0, 0.75, 0.8)
+    ensure_half_exp(tb._lib, torch.cuda.current_device())  # (as the search loop does)
+    return tb
+
+
+def test_half_exp_table_is_numpy():
+    """The float16 exp table the glue kernels read is numpy's own np.exp of every half (the SIMD half
+    loop where numpy has one); where it differs from float32 exp rounded to half is host-dependent."""
+    from mazero_amd.mcts_sampled import half_exp_table
+
+    t = half_exp_table()
+    assert t.dtype == np.uint16 and t.shape == (65536,)
+    x = np.arange(65536, dtype=np.uint16).view(np.float16)
+    fin = np.isfinite(x)
+    with np.errstate(all="ignore"):
+        np.testing.assert_array_equal(t[fin], np.exp(x[fin]).view(np.uint16))
 
 
 @pytest.mark.gpu
