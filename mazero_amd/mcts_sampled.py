@@ -200,18 +200,26 @@ class _SearchLoop:
         tb.prepare_selection_device(r[0], r[1], r[2], r[3], K, eps, r[4], c2, c1, disc, out=self.sel)
         act = self.sel[2]
         leaf = self.root  # simulation 0 selects a child of every root: its parent is the root (slot 0)
+        # One autocast context around the whole loop, its cast cache on: each fp32 weight is cast to
+        # float16 once per search instead of once per simulation (the reference enters autocast per
+        # simulation, mcts_sampled.py:150, so it casts every weight S times; the casts are identical).
+        # The context opens and closes inside a capture, so the cached casts live in the graph's pool.
+        with torch.autocast("cuda", cache_enabled=True):
+            self._simulations(model, lib, h, leaf, act, B, A, N, cur, K, S, c2, c1, disc, tau)
+
+    def _simulations(self, model, lib, h, leaf, act, B, A, N, cur, K, S, c2, c1, disc, tau):
+        tb = self.tb
         for s in range(S):
-            with torch.autocast("cuda", cache_enabled=False):
-                if cur + 1 < N:  # later agents' actions from the leaf policy, :136-145
-                    pred_logits, _ = model.prediction(leaf)
-                    pred_logits = pred_logits.contiguous()
-                    ptr, dt = C.c_void_p(pred_logits.data_ptr()), _dtype_code(pred_logits)
-                else:
-                    ptr, dt = None, MZ_DT_F32
-                check(lib, lib.mz_joint_action(h, ptr, dt, N, cur, C.c_void_p(self.fac.data_ptr()),
-                                               self.fac.shape[1], C.c_void_p(act.data_ptr()),
-                                               C.c_void_p(self.joint.data_ptr())), "joint_action")
-                next_h, reward, value, logits = SampledMCTS._recurrent(model, leaf, self.joint)  # :150-156
+            if cur + 1 < N:  # later agents' actions from the leaf policy, :136-145
+                pred_logits, _ = model.prediction(leaf)
+                pred_logits = pred_logits.contiguous()
+                ptr, dt = C.c_void_p(pred_logits.data_ptr()), _dtype_code(pred_logits)
+            else:
+                ptr, dt = None, MZ_DT_F32
+            check(lib, lib.mz_joint_action(h, ptr, dt, N, cur, C.c_void_p(self.fac.data_ptr()),
+                                           self.fac.shape[1], C.c_void_p(act.data_ptr()),
+                                           C.c_void_p(self.joint.data_ptr())), "joint_action")
+            next_h, reward, value, logits = SampledMCTS._recurrent(model, leaf, self.joint)  # :150-156
             nh = next_h.reshape(B, -1)
             chain = K == 1
             if chain:

@@ -7,7 +7,7 @@
 The two FillFunctor<short> marks bracket bench_search.py's timed region (env steps of graph-replayed
 searches, each followed by the host readback).  Every dispatch between them is classified by name:
   tree    the mz kernels of the tree library (k_prepare, k_chain*, k_tree, k_step, k_readback, ...)
-  glue    the driver glue (k_policy_glue, k_joint_action)
+  glue    the driver glue (k_policy_glue, k_joint_action, k_root_glue)
   copies  torch copy / fill kernels (the hidden-state pool copy, input uploads, dtype casts)
   model   everything else (the network's GEMMs, norms, activations, reductions)
 Per simulation = the window's totals / (steps x agents x sims).  `span` is the window's wall time on
@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from trace_window import load_trace, short, window  # noqa: E402
 
 TREE = ("k_prepare", "k_chain", "k_tree", "k_step", "k_readback", "k_copy_words", "k_set_word", "k_gather")
-GLUE = ("k_policy_glue", "k_joint_action")
+GLUE = ("k_policy_glue", "k_joint_action", "k_root_glue")
 COPY_HINTS = ("copy", "Copy", "fill", "Fill", "cast", "Cast")
 
 
