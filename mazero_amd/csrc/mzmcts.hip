@@ -159,6 +159,10 @@ struct PrepArgs {
 struct Params {
     Geo g;
     Dev d;
+    // std::mt19937 seeding checkpoints (seed_table): row v holds x_{16j}(v), j < 39, for v < cp_n;
+    // null: k_prepare runs the seeding chain
+    const unsigned *cp;
+    unsigned cp_n;
 };
 
 // Arena offsets of every array a k_step launch reads in its first round, as a function of the
@@ -880,10 +884,32 @@ __device__ __forceinline__ unsigned mt_temper(unsigned z) {
     return z;
 }
 
+// std::mt19937::seed(v) is the chain x_0 = v, x_i = 1812433253 (x_{i-1} ^ (x_{i-1} >> 30)) + i,
+// 623 dependent steps (~5 us per tree on the scalar unit, most of k_prepare).  Its state is the
+// previous word alone, so the words x_{16j} split it into 39 independent 16-step pieces: the
+// per-device table (seed_table) holds them for every v below its size, and k_prepare's lanes
+// replay the pieces in parallel.  Row v: x_{16j}(v) for j < 39 (word 39 unused, 160-byte rows).
+constexpr int kSeedStep = 16, kSeedRow = 40;
+static_assert(kMtN % kSeedStep == 0 && kMtN / kSeedStep < kSeedRow, "seeding checkpoints");
+
+__global__ __launch_bounds__(256) void k_seed_table(unsigned *cp, unsigned n) {
+    const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    unsigned *row = cp + (size_t)v * kSeedRow;
+    unsigned x = v;
+    row[0] = x;
+    for (int i = 1; i < kMtN; ++i) {
+        x = 1812433253u * (x ^ (x >> 30)) + (unsigned)i;
+        if (i % kSeedStep == 0) row[i / kSeedStep] = x;
+    }
+    row[kSeedRow - 1] = 0u;
+}
+
 __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm, PrepArgs a) {
     const Geo g = prm->g;
     const Dev d = prm->d;
     __shared__ unsigned mt[kMtN];
+    __shared__ unsigned mt2[kMtN];
     __shared__ unsigned w0[kMtN];
     const int t = blockIdx.x;
     const int tid = threadIdx.x;
@@ -891,7 +917,27 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     // error also stays in its header, and every later kernel re-reports the errors of dead trees,
     // so an error raised by another block before this store is not lost.
     if (t == 0 && tid == 0) *d.err() = 0;
-#ifndef MZ_SEED_LOOP
+    const unsigned seed_v = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
+    const unsigned *cp = prm->cp;
+    if (cp && seed_v < prm->cp_n) {
+        // the seeding chain from the checkpoints: lane j replays words 16j .. 16j + 15
+        if (tid < kMtN / kSeedStep) {
+            const int i0 = kSeedStep * tid;
+            unsigned x = cp[(size_t)seed_v * kSeedRow + tid];
+            mt[i0] = x;
+#pragma unroll
+            for (int i = 1; i < kSeedStep; ++i) {
+                x = 1812433253u * (x ^ (x >> 30)) + (unsigned)(i0 + i);
+                mt[i0 + i] = x;
+            }
+        }
+    } else
+#if defined(MZ_ABL_NOSEED)  // ablation (timing experiments only): no seeding chain
+    if (tid < kWave) {
+        const unsigned x = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
+        for (int i = tid; i < kMtN; i += kWave) mt[i] = x + (unsigned)i;
+    }
+#elif !defined(MZ_SEED_LOOP)
     if (tid < kWave) {
         // std::mt19937::seed (sequential by definition) on the scalar unit: 4 SALU operations per
         // word, word i into lane i % 64 of VGPR i / 64 (mt_seed.inc, scripts/gen_mt_seed.py), then
@@ -933,36 +979,40 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
 #ifdef MZ_ABL_NOTWIST  // ablation (timing experiments only): no twist / tempering
     nb = 0;
 #endif
+    // One twist per 624-word block (std::mt19937::_M_gen_rand), one barrier each: thread k < 227
+    // computes the three words k, k + 227, k + 454 of the new state in registers.  Word k uses old
+    // words only; word k + 227 uses new word k (its x[k + 227 - 227]); word k + 454 uses new word
+    // k + 227; the last word (623, thread 169) also uses new word 0, which it recomputes.  The old
+    // state is read from one LDS buffer and the new one written to the other.
+    unsigned *cur = mt, *nxt = mt2;
     for (int blk = 0; blk < nb; ++blk) {
-        unsigned v = 0;
-        // k in [0, 227): x[k] = x[k+397] ^ twist(x[k], x[k+1])       (all old)
-        if (tid < 227) v = mt[tid + 397] ^ mt_twist(mt[tid], mt[tid + 1]);
-        lds_barrier();
-        if (tid < 227) mt[tid] = v;
-        lds_barrier();
-        // k in [227, 454): x[k] = x[k-227](new) ^ twist(x[k], x[k+1])(old)
-        {
-            const int k = 227 + tid;
-            if (k < 454) v = mt[k - 227] ^ mt_twist(mt[k], mt[k + 1]);
-            lds_barrier();
-            if (k < 454) mt[k] = v;
-            lds_barrier();
-        }
-        // k in [454, 624): x[k] = x[k-227](new) ^ twist(x[k], x[k+1 or 0(new)])
-        {
-            const int k = 454 + tid;
-            if (k < kMtN) v = mt[k - 227] ^ mt_twist(mt[k], (k == kMtN - 1) ? mt[0] : mt[k + 1]);
-            lds_barrier();
-            if (k < kMtN) mt[k] = v;
-            lds_barrier();
-        }
         unsigned *dst = d.R() + (size_t)t * g.W + (size_t)blk * kMtN;
-        for (int k = tid; k < kMtN; k += blockDim.x) {
-            const unsigned z = mt_temper(mt[k]);
-            dst[k] = z;
-            if (blk == 0) w0[k] = z;
+        if (tid < 227) {
+            const int k = tid;
+            const unsigned n0 = cur[k + 397] ^ mt_twist(cur[k], cur[k + 1]);
+            const unsigned n1 = n0 ^ mt_twist(cur[k + 227], cur[k + 228]);
+            nxt[k] = n0;
+            nxt[k + 227] = n1;
+            const unsigned z0 = mt_temper(n0), z1 = mt_temper(n1);
+            dst[k] = z0;
+            dst[k + 227] = z1;
+            if (blk == 0) {
+                w0[k] = z0;
+                w0[k + 227] = z1;
+            }
+            if (k < kMtN - 454) {
+                const unsigned nx = (k + 455 < kMtN) ? cur[k + 455] : (cur[397] ^ mt_twist(cur[0], cur[1]));
+                const unsigned n2 = n1 ^ mt_twist(cur[k + 454], nx);
+                nxt[k + 454] = n2;
+                const unsigned z2 = mt_temper(n2);
+                dst[k + 454] = z2;
+                if (blk == 0) w0[k + 454] = z2;
+            }
         }
         lds_barrier();
+        unsigned *tmp = cur;
+        cur = nxt;
+        nxt = tmp;
     }
     if (tid >= kWave) return;
 
@@ -5322,6 +5372,52 @@ int fail(int code, const std::string &m) {
 
 int round16(int x) { return (x + 15) & ~15; }
 
+// The per-device table of std::mt19937 seeding checkpoints (k_seed_table), shared by every handle
+// of the device: rows for every seed value v = random_seed * 2333 + root index (cnode.cpp:574) below
+// its size, sized for random_seed < 256 (np_random.choice(256), mcts_sampled.py:89) and at least
+// 4096 roots (~97 MB).  Built once (a few ms), grown when a handle's roots need more; an outgrown
+// table stays allocated (handles made before it, and graphs they recorded, read it).  Seeds outside
+// the table take the sequential chain.
+struct SeedTable {
+    unsigned *p = nullptr;
+    unsigned n = 0;
+};
+constexpr int kSeedTabDevices = 64;
+std::mutex g_seed_mu;
+SeedTable g_seed_tab[kSeedTabDevices];
+
+void seed_table(int dev, unsigned long long need, const unsigned **cp, unsigned *cp_n) {
+    *cp = nullptr;
+    *cp_n = 0;
+    if (dev < 0 || dev >= kSeedTabDevices) return;
+    std::lock_guard<std::mutex> lk(g_seed_mu);
+    SeedTable &st = g_seed_tab[dev];
+    if (st.n < need) {
+        unsigned long long n = 256ull * 2333ull + 4096ull;
+        if (n < need) n = need;
+        if (n > 0xffffffffull) n = 0xffffffffull;
+        void *p = nullptr;
+        hipStream_t s = nullptr;
+        bool ok = hipMalloc(&p, (size_t)n * kSeedRow * sizeof(unsigned)) == hipSuccess;
+        ok = ok && hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(k_seed_table, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (unsigned *)p,
+                               (unsigned)n);
+            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(s) == hipSuccess;
+        }
+        if (s) (void)hipStreamDestroy(s);
+        if (!ok) {  // (no table: k_prepare runs the chain)
+            if (p) (void)hipFree(p);
+            (void)hipGetLastError();
+            return;
+        }
+        st.p = (unsigned *)p;
+        st.n = (unsigned)n;
+    }
+    *cp = st.p;
+    *cp_n = st.n;
+}
+
 bool getenv_flag(const char *name) {
     const char *v = std::getenv(name);
     return v && v[0] == '1';
@@ -6070,7 +6166,12 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     // (pools above 256 nodes keep k_chain: wave 1 holds the chain's records in registers, 8 per 64 nodes)
     if (b->chain_nc > 0 && b->chain_nc <= 256 && b->P < 1024 && b->PS < 1024 && !getenv_flag("MZ_CHAIN_V2"))
         b->chain3_nc = b->chain_nc;
-    const Params host_params{b->geo, b->dev};
+    const unsigned *seed_cp = nullptr;
+    unsigned seed_cp_n = 0;
+    if (!getenv_flag("MZ_NO_SEED_TABLE"))
+        seed_table(b->device, 255ull * 2333ull + (unsigned long long)(root_offset > 0 ? root_offset : 0) + (unsigned long long)B,
+                   &seed_cp, &seed_cp_n);
+    const Params host_params{b->geo, b->dev, seed_cp, seed_cp_n};
     std::vector<float> lp(b->PS + 1 + kWave, 0.f);
     lp[0] = 1.0f;
     for (int k = 1; k < b->PS + 1; ++k) lp[k] = lp[k - 1] * lam;  // lam_pow chain (utils.cpp:25-27)

@@ -210,6 +210,32 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
 
 
+@pytest.mark.parametrize("seeding", ["table", "chain", "beyond_table"])
+@pytest.mark.parametrize("K", [1, 5])
+def test_seeding_paths_vs_port(gpu_lib, port_lib, seeding, K, monkeypatch):
+    """k_prepare seeds each tree's mt19937 (cnode.cpp:574) from the per-device checkpoint table
+    (seed values below its size), by the sequential chain with MZ_NO_SEED_TABLE=1 (read at
+    mz_create), and by the chain for a seed value beyond the table (random_seed 100000: v =
+    233,300,000 + i).  Every selection and readback against the CPU port; 2 x 624 + 102 words of
+    engine stream are consumed at S = 50, so the twist's block boundaries are crossed too."""
+    from dataclasses import replace
+
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    rng = np.random.default_rng(4242 + K)
+    inp = make_search_inputs(rng, 128, 9, 50, legal_zero_frac=0.2)
+    if seeding == "beyond_table":
+        inp = replace(inp, seed=100000)
+    exp = run_search(make_tb(port_lib, inp, K, {}), inp, K, {})
+    if seeding == "chain":
+        monkeypatch.setenv("MZ_NO_SEED_TABLE", "1")
+    tb = make_tb(gpu_lib, inp, K, {})
+    monkeypatch.delenv("MZ_NO_SEED_TABLE", raising=False)
+    out, _ = run_fused(tb, to_device(inp), K, {})
+    exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, exp, f"gpu seeding={seeding} K={K} ")
+
+
 def test_chain_v2_on_reference_fixture(gpu_lib, monkeypatch):
     """MZ_CHAIN_V2=1 (read at mz_create) sends K = 1 pools of <= 256 nodes to the round-2 k_chain
     instead of k_chain3: the 3m K = 1 BASELINE fixture through it, against the reference."""
