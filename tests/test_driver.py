@@ -203,6 +203,72 @@ def test_policy_glue_matches_numpy(dtype, A):
     np.testing.assert_array_equal(gb.view(np.uint32), eb.reshape(B, A).view(np.uint32))
 
 
+def _half_exp_exceptions() -> np.ndarray:
+    """Non-positive float16 values d where this host's np.exp(d) differs from np.exp in float32
+    rounded to half (numpy's SIMD half loop; the softmax evaluates exp(x - max) <= 1)."""
+    x = np.arange(1 << 16, dtype=np.uint16).view(np.float16)
+    x = x[np.isfinite(x) & (x <= 0)]
+    with np.errstate(all="ignore"):
+        diff = np.exp(x).view(np.uint16) != np.exp(x.astype(np.float32)).astype(np.float16).view(np.uint16)
+    return x[diff]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("A", [9, 15])
+def test_glue_half_exp_exceptions(A):
+    """Rows built so that x - max lands on the half values where numpy's float16 exp is not float32
+    exp rounded to half: mz_policy_glue and mz_root_glue against numpy through the exp table."""
+    import torch
+
+    from mazero_amd._capi import MZ_DT_F16, check
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import NetworkOutput, SearchConfig
+
+    exc = _half_exp_exceptions()
+    if exc.size == 0:
+        pytest.skip("this host's numpy evaluates float16 exp as float32 exp rounded (no exceptions)")
+    B, N, cur = 256, 3, 2
+    rng = np.random.default_rng(11 + A)
+    logits = rng.standard_normal((B, N, A)).astype(np.float16)
+    for i in range(B):  # the row's max is 0, the other entries exception values (and a few normal ones)
+        row = rng.choice(exc, size=A)
+        row[rng.integers(A)] = 0.0
+        row[rng.integers(A)] = np.float16(rng.standard_normal()) - np.float16(4.0)
+        logits[i, cur] = row
+    dev = torch.device("cuda", 0)
+    tb = _handle(B, A)
+    x = torch.from_numpy(logits).to(dev)
+    probs, beta = torch.empty(B, A, device=dev), torch.empty(B, A, device=dev)
+    tb._sync_stream()
+    check(tb._lib, tb._lib.mz_policy_glue(tb._h, C.c_void_p(x.data_ptr()), MZ_DT_F16, N * A, cur * A, 1.0,
+                                          C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr())), "policy_glue")
+    with np.errstate(all="ignore"):
+        ep, eb = _numpy_policy_glue(logits[:, cur, :].reshape(B, 1, A))
+    np.testing.assert_array_equal(probs.cpu().numpy().view(np.uint32), ep.reshape(B, A).view(np.uint32))
+    np.testing.assert_array_equal(beta.cpu().numpy().view(np.uint32), eb.reshape(B, A).view(np.uint32))
+    # the root preprocessing (softmax, then an int64 mask and the noise)
+    legal = (rng.random((B, N, A)) >= 0.2).astype(np.int64)
+    legal[..., 0] = 1
+    out = NetworkOutput(torch.zeros(B, 4, device=dev), rng.standard_normal((B, 1)).astype(np.float32),
+                        rng.standard_normal((B, 1)).astype(np.float32), logits)
+    cfg = SearchConfig(action_space_size=A)
+    m_host, m_dev = SampledMCTS(cfg, np.random.RandomState(5)), SampledMCTS(cfg, np.random.RandomState(5))
+    for lg in (None, legal):
+        (rr, rv, rp, rb, eps, rn), _ = m_host.root_inputs(out, cur, lg, True, 1.0)
+        arrays, mode, eps_d, _ = m_dev.root_raw(out, cur, lg, True)
+        t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in arrays.items()}
+        p2, b2, n2 = (torch.empty(B, A, device=dev) for _ in range(3))
+        tb._sync_stream()
+        lgt = t.get("legal")
+        check(tb._lib, tb._lib.mz_root_glue(tb._h, C.c_void_p(t["logits"].data_ptr()), mode[0], A, 0,
+                                            None if lgt is None else C.c_void_p(lgt.data_ptr()), A,
+                                            C.c_void_p(t["noise"].data_ptr()), float(eps_d), 1.0,
+                                            C.c_void_p(p2.data_ptr()), C.c_void_p(b2.data_ptr()),
+                                            C.c_void_p(n2.data_ptr())), "root_glue")
+        for got, exp in ((p2, rp), (b2, rb), (n2, rn)):
+            np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), exp.reshape(B, A).view(np.uint32))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["float32", "float16"])
 def test_joint_action_matches_numpy(dtype):
