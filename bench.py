@@ -118,6 +118,8 @@ class HipLeg:
 
         B = host_inputs[0].B
         self.args, self.B, self.lib, self.stream = args, B, lib, stream
+        # the last expansion and the readback in one launch (an older experiment build may lack it)
+        self.fused_rb = hasattr(lib, "mz_expand_backup_readback")
         N, A = CONFIGS[args.map]
         S, K = args.sims, args.sampled_times
         self.N, self.A, self.S, self.K, self.H = N, A, S, K, N * HIDDEN_PER_AGENT
@@ -160,10 +162,16 @@ class HipLeg:
             if s + 1 < S:
                 tb.expansion_backup_selection_device(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s],
                                                      c2, c1, out=out, pool=sd["pool"], gather_out=sd["leaf"])
+            elif self.fused_rb:
+                # the last expansion writes the search outputs too (mz_expand_backup_readback): they stay on
+                # the device (mcts_sampled.py:176-191)
+                tb.expansion_backup_readback_device(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s],
+                                                    readback_discount=g,
+                                                    out=dict(values=sd["values"], marginal_visit_count=sd["visits"]))
             else:
                 tb.batch_expansion_and_backup(s + 1, g, K, sd["r"][s], sd["v"][s], sd["p"][s], sd["b"][s])
-        # search outputs stay on the device (mcts_sampled.py:176-191): one readback launch
-        tb.get_roots_device(g, values=sd["values"], marginal_visit_count=sd["visits"])
+        if not self.fused_rb:  # search outputs stay on the device (mcts_sampled.py:176-191): one readback launch
+            tb.get_roots_device(g, values=sd["values"], marginal_visit_count=sd["visits"])
 
     def env_step(self):
         for sd in self.searches:  # agents searched sequentially (selfplay_worker.py:196-211)

@@ -42,6 +42,25 @@ int mz_reseed(mz_batch *b, uint32_t random_seed);
  * fresh input copies is a new search.) */
 int mz_state_changed(mz_batch *b);
 
+/* The search's last expansion + back-propagation (mz_expand_backup with device inputs,
+ * mcts_sampled.py:168 at s = S - 1) and the readback of every root output (mz_get_roots_device,
+ * mcts_sampled.py:176-191, cnode.cpp:672-781) in one launch: the chain and tree kernels write the
+ * outputs from their final state; the handle's other kernels are followed by the readback kernel.
+ * out != NULL: the caller's device buffers (as mz_get_roots_device); out == NULL: the handle's packed
+ * readback buffer, so that the host getters that follow only copy it (one device->host copy).
+ * readback_discount is the q values' discount (get_roots_sampled_qvalues).  The destinations are
+ * kept in one of eight device descriptor slots per handle, uploaded at their first use; a first use
+ * inside a graph capture, or a ninth set of destinations, takes the two-launch form. */
+int mz_expand_backup_readback(mz_batch *b, int hidden_state_index_x, float discount, int sampled_times,
+                              const float *rewards, const float *values, const float *policy, const float *beta,
+                              float readback_discount, const mz_readback_out *out);
+
+/* After replaying a captured graph whose last mz_* launch on this handle was
+ * mz_expand_backup_readback(..., out = NULL): the trees changed (as mz_state_changed) and the
+ * packed readback buffer holds their outputs for `discount`, so the host getters copy it without
+ * a readback launch. */
+int mz_readback_ready(mz_batch *b, float discount);
+
 /* Policy glue of one simulation (mcts_sampled.py:156-161 and 169-170).
  * logits: the network's policy logits [B, num_agents, A] (row stride `row_stride` elements,
  * the current agent's A logits start at element `col_offset` of a row), dtype `dtype`.

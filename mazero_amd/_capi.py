@@ -114,6 +114,8 @@ DRIVER_SIGNATURES = {
     "mz_graph_census": (_i, [_p, C.POINTER(_i), C.POINTER(_i)]),
     "mz_fused_kernel": (_i, [_p, C.c_char_p, _i]),
     "mz_set_half_exp_table": (_i, [_p]),
+    "mz_expand_backup_readback": (_i, [_p, _i, _f, _i, _p, _p, _p, _p, _f, _p]),
+    "mz_readback_ready": (_i, [_p, _f]),
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 

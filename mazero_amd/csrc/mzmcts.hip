@@ -296,6 +296,82 @@ __device__ __forceinline__ int act_of(int y) { return (y >> 8) & 0xff; }
 __device__ __forceinline__ int md_of(int y) { return (int)((unsigned)y >> 16) - 1; }
 __device__ __forceinline__ int pack_y(int nc, int act, int md) { return nc | (act << 8) | ((md + 1) << 16); }
 
+// --------------------------------------------------------------------------------------------
+// Readbacks (cnode.cpp:672-781, cytree.pyx:93-247): root value, marginal visit counts / priors,
+// root degree and every per-child field of the root, field-major (4-byte words):
+//   [B] root value | [B*A] marginal visits | [B*A] marginal priors | [B] degree |
+//   MZ_F_COUNT x [B*Wd] per-child fields padded with zeros to Wd = max degree
+// Destinations: the handle's packed buffer (readback_dev) or the caller's device buffers
+// (mz_get_roots_device); a null field is not written.  Per-child fields are [B][Wd(*N)] either way.
+// --------------------------------------------------------------------------------------------
+struct RbPtrs {
+    float *values;  // [B]
+    int *mv;        // [B][N*A] marginal visit counts
+    float *mp;      // [B][N*A] marginal priors
+    int *deg;       // [B] root degrees
+    int *f[MZ_F_COUNT];
+};
+// A fused readback's destinations and constants, in device memory (mz_expand_backup_readback): the
+// search's last expansion kernel reads it (SEL = false launches pass it in their gather_out slot)
+struct RbDesc {
+    RbPtrs o;
+    float disc;  // the discount of the q values (cnode.cpp:165)
+    int Wd;      // per-child field width
+    int pad[2];
+};
+
+// Tree t's readback from its final records, one lane per root child (lane l < nc: child fc + l):
+// ra = the root's {visit, prior, value, reward}; ca / cb / cd = the child's {visit, prior, value,
+// reward} / {first_child, nc|act|md, pred_value, hsx} / {pred_prob, beta, beta_hat}.  jt: the
+// children's joint actions [nc][N] (N > 1), else unused.
+__device__ __forceinline__ void readback_emit(const RbPtrs &o, float disc, int Wd, int t, int A, int N, int nc, int4 ra,
+                                              int4 ca, int4 cb, float4 cd, const unsigned char *jt) {
+    const int l = threadIdx.x & 63;
+    const int NA = N * A;
+    if (l == 0) {
+        if (o.values) o.values[t] = (nc > 0) ? i2f(ra.z) : 0.f;
+        if (o.deg) o.deg[t] = nc;
+    }
+    const bool has = l < nc;
+    const int act = act_of(cb.y);
+    // marginal visit counts / priors (cnode.cpp:69-91): cell (agent j, action a) collects, in child
+    // order, every child whose action for agent j is a
+    if (o.mv || o.mp)
+        for (int cell = l; cell < NA; cell += 64) {
+            const int j = cell / A, av = cell - j * A;
+            int mv = 0;
+            float mp = 0.f;
+            for (int c = 0; c < nc; ++c) {
+                const int aj = (N == 1) ? rl(act, c) : (int)jt[c * N + j];
+                const int vj = rl(ca.x, c);
+                const float pj = rlf(i2f(ca.y), c);
+                if (aj == av) {
+                    mv += vj;
+                    mp += pj;
+                }
+            }
+            if (o.mv) o.mv[(size_t)t * NA + cell] = mv;
+            if (o.mp) o.mp[(size_t)t * NA + cell] = mp;
+        }
+    if (l < Wd) {
+        const size_t r = (size_t)t * Wd + l;
+        const float val = i2f(ca.z);  // CNode::value(): 0 when not expanded (stored that way)
+        const float rew = i2f(ca.w);
+        if (int *fa = o.f[MZ_F_ACTIONS]) {
+            if (N == 1)
+                fa[r] = has ? act : 0;
+            else
+                for (int i = 0; i < N; ++i) fa[r * N + i] = has ? (int)jt[l * N + i] : 0;
+        }
+        if (o.f[MZ_F_VISIT_COUNT]) o.f[MZ_F_VISIT_COUNT][r] = has ? ca.x : 0;
+        const float fv[MZ_F_COUNT] = {0.f, 0.f, cd.x, cd.y, cd.z, i2f(ca.y), cd.z / cd.y * cd.x, i2f(cb.z), val, rew,
+                                      rew + disc * val};
+#pragma unroll
+        for (int f = MZ_F_PRED_PROBS; f < MZ_F_COUNT; ++f)
+            if (o.f[f]) ((float *)o.f[f])[r] = has ? fv[f] : 0.f;
+    }
+}
+
 // Wait for this wave's memory traffic (LDS-DMA included via vmcnt) / LDS traffic; compiler fence.
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -3611,6 +3687,29 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         hp->tame = tame;
         hp->leaf = (err || !SEL) ? h.leaf : c;
     }
+    if constexpr (!SEL) {
+        // the fused readback (mz_expand_backup_readback, include/mzdriver.h): the search's outputs
+        // from this launch's final records.  Wave 1 left every chain node's new {visit, prior, value,
+        // reward} in sA (read after the barrier above); the structure records come from HBM but the
+        // leaf's, rewritten above, and the root children's probabilities from HBM (written at prepare)
+        const RbDesc *rbd = (const RbDesc *)(const void *)iop->gather_out;
+        if (rbd && !err) {
+            const int4 rbn = uni4(d.Bn()[nb]);
+            const int nc = nc_of(rbn.y), fc = rbn.x;
+            d.o_D = pl->d.o_D;
+            const int md = md_of(leaf_b.y) < 0 ? 0 : md_of(leaf_b.y);
+            const int4 leaf_new = make_int4(c, pack_y(1, act_of(leaf_b.y), md), f2i(v_in), hsx);
+            int4 ca = make_int4(0, 0, 0, 0), cb = ca;
+            float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (l < nc) {
+                const int n = fc + l;
+                ca = sA[n];
+                cb = (n == leaf) ? leaf_new : d.Bn()[nb + n];
+                cd = d.D()[nb + n];
+            }
+            readback_emit(rbd->o, rbd->disc, rbd->Wd, t, A, 1, nc, sA[0], ca, cb, cd, nullptr);
+        }
+    }
     stamp(ts, 6);
     if (MZ_STAMPS && l >= MZ_S_CYC_HEADER && l < MZ_S_COUNT) {
         d.o_stats = pl->d.o_stats;
@@ -5137,6 +5236,33 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             hp->leaf = (err || !SEL) ? h.leaf : x;
         }
     }
+    if constexpr (!SEL) {
+        // the fused readback (mz_expand_backup_readback, include/mzdriver.h): the search's outputs
+        // from the state after barrier (2) -- the staged records (sA, sB), the path nodes' new value
+        // and reward (sAz; flagged in sFl, one more visit), the leaf's new structure record (sB) --
+        // and the root children's probabilities from HBM (written at prepare)
+        const RbDesc *rbd = (const RbDesc *)(const void *)gather_out;
+        if (rbd && !err) {
+            auto upd = [&](int n) {
+                int4 a = sA[n];
+                if (sFl[n]) {
+                    const float2 az = sAz[n];
+                    a = make_int4(a.x + 1, a.y, f2i(az.x), f2i(az.y));
+                }
+                return a;
+            };
+            const int4 rbn = uni4(sB[0]);
+            const int nc = nc_of(rbn.y), fc = rbn.x;
+            int4 ca = make_int4(0, 0, 0, 0), cb = ca;
+            float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (l < nc) {
+                ca = upd(fc + l);
+                cb = sB[fc + l];
+                cd = d.D()[nb + fc + l];
+            }
+            readback_emit(rbd->o, rbd->disc, rbd->Wd, t, A, 1, nc, upd(0), ca, cb, cd, nullptr);
+        }
+    }
     if (gath_lds) {
         wait_vm();
 #ifdef MZ_SPANS_EPI
@@ -5213,29 +5339,12 @@ __global__ __launch_bounds__(64) void k_gather(const char *pool, long long strid
     }
 }
 
-// --------------------------------------------------------------------------------------------
-// Readbacks (cnode.cpp:672-781 over CNode getters 69-171), all fields in one pass.  Packed
-// field-major output (4-byte words):
-//   [B] root value | [B*A] marginal visits | [B*A] marginal priors | [B] degree |
-//   MZ_F_COUNT x [B*Wd] per-child fields padded with zeros to Wd = max degree
-// --------------------------------------------------------------------------------------------
-// Destinations of one k_readback launch: the handle's packed buffer (readback_dev) or the caller's
-// device buffers (mz_get_roots_device); a null field is not written.  Per-child fields are
-// [B][Wd(*N)] either way.
-struct RbPtrs {
-    float *values;  // [B]
-    int *mv;        // [B][N*A] marginal visit counts
-    float *mp;      // [B][N*A] marginal priors
-    int *deg;       // [B] root degrees
-    int *f[MZ_F_COUNT];
-};
-
+// Readbacks (cnode.cpp:672-781 over CNode getters 69-171), all fields in one pass (readback_emit)
 __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm, float disc, int Wd, RbPtrs o) {
     const Geo g = prm->g;
     const Dev d = prm->d;
     const int t = blockIdx.x;
     const int l = threadIdx.x;
-    const int A = g.A;
     const size_t nb = (size_t)t * g.P;
     const int4 ra = d.A()[nb];
     const int4 rbn = d.Bn()[nb];
@@ -5245,57 +5354,15 @@ __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm,
         const int herr = d.hdr()[t].err;  // dead trees re-report their error (see k_prepare)
         if (l == 0 && herr) atomicOr(d.err(), herr);
     }
-    const int N = g.N, NA = g.NA;
-    if (l == 0) {
-        if (o.values) o.values[t] = (nc > 0) ? i2f(ra.z) : 0.f;
-        if (o.deg) o.deg[t] = nc;
-    }
-    const bool has = l < nc;
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
     float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (has) {
+    if (l < nc) {
         ca = d.A()[nb + fc + l];
         cb = d.Bn()[nb + fc + l];
         cd = d.D()[nb + fc + l];
     }
-    const int act = act_of(cb.y);
-    const unsigned char *jt = d.J() + (size_t)t * g.JP + (size_t)fc * N;  // joint actions (N > 1)
-    // marginal visit counts / priors (cnode.cpp:69-91): cell (agent j, action a) collects, in child
-    // order, every child whose action for agent j is a
-    if (o.mv || o.mp)
-        for (int cell = l; cell < NA; cell += kWave) {
-            const int j = cell / A, av = cell - j * A;
-            int mv = 0;
-            float mp = 0.f;
-            for (int c = 0; c < nc; ++c) {
-                const int aj = (N == 1) ? rl(act, c) : (int)jt[c * N + j];
-                const int vj = rl(ca.x, c);
-                const float pj = rlf(i2f(ca.y), c);
-                if (aj == av) {
-                    mv += vj;
-                    mp += pj;
-                }
-            }
-            if (o.mv) o.mv[(size_t)t * NA + cell] = mv;
-            if (o.mp) o.mp[(size_t)t * NA + cell] = mp;
-        }
-    if (l < Wd) {
-        const size_t r = (size_t)t * Wd + l;
-        const float val = i2f(ca.z);  // CNode::value(): 0 when not expanded (stored that way)
-        const float rew = i2f(ca.w);
-        if (int *fa = o.f[MZ_F_ACTIONS]) {
-            if (N == 1)
-                fa[r] = has ? act : 0;
-            else
-                for (int i = 0; i < N; ++i) fa[r * N + i] = has ? (int)jt[l * N + i] : 0;
-        }
-        if (o.f[MZ_F_VISIT_COUNT]) o.f[MZ_F_VISIT_COUNT][r] = has ? ca.x : 0;
-        const float fv[MZ_F_COUNT] = {0.f, 0.f, cd.x, cd.y, cd.z, i2f(ca.y), cd.z / cd.y * cd.x, i2f(cb.z), val, rew,
-                                      rew + disc * val};
-#pragma unroll
-        for (int f = MZ_F_PRED_PROBS; f < MZ_F_COUNT; ++f)
-            if (o.f[f]) ((float *)o.f[f])[r] = has ? fv[f] : 0.f;
-    }
+    const unsigned char *jt = d.J() + (size_t)t * g.JP + (size_t)fc * g.N;  // joint actions (N > 1)
+    readback_emit(o, disc, Wd, t, g.A, g.N, nc, ra, ca, cb, cd, jt);
 }
 
 }  // namespace
@@ -5318,6 +5385,12 @@ struct mz_batch {
     float *in_dev = nullptr;  // host-input staging [B*(2+3A)]
     int *sel_dev = nullptr;   // select output staging [3B]
     int *rb_dev = nullptr;    // packed readback
+    // fused readbacks (mz_expand_backup_readback): descriptor slots in device memory and their host
+    // copies (a slot is uploaded once and never rewritten, so a recorded launch may keep reading it)
+    RbDesc *rb_desc_dev = nullptr;
+    RbDesc rb_desc_host[8];
+    int rb_desc_n = 0;
+    bool fused_rb = true;
     size_t rb_words = 0;
     int *rb_host = nullptr;     // packed readback, host mirror (in the pinned stage)
     bool rb_valid = false;      // rb_host mirrors the current tree state
@@ -5910,11 +5983,8 @@ int flush_pending(mz_batch *b) {
     return stage_consumed(b);
 }
 
-// Packed readback computed on the device (stream-ordered, no synchronisation).
-int readback_dev(mz_batch *b, float disc) {
-    int rc = flush_pending(b);
-    if (rc) return rc;
-    if (b->rb_dev_valid && b->rb_disc == disc) return MZ_OK;
+// the packed readback buffer's fields
+RbPtrs packed_rb(const mz_batch *b) {
     RbPtrs o;
     int *rb = b->rb_dev;
     const size_t n = (size_t)b->B * b->NA;
@@ -5923,6 +5993,44 @@ int readback_dev(mz_batch *b, float disc) {
     o.mp = (float *)(rb + b->B + n);
     o.deg = rb + rb_deg_base(b);
     for (int f = 0; f < MZ_F_COUNT; ++f) o.f[f] = rb + rb_field_base(b, f);
+    return o;
+}
+
+// The device slot holding a fused readback's descriptor (destinations, discount, width), uploaded
+// on first use; null when every slot is taken by other destinations, or when the first use comes
+// inside a graph capture (the upload is eager work): the caller then launches k_readback itself.
+const RbDesc *rb_desc_slot(mz_batch *b, const RbPtrs &o, float disc) {
+    constexpr int kSlots = (int)(sizeof(b->rb_desc_host) / sizeof(RbDesc));
+    RbDesc want;
+    std::memset(&want, 0, sizeof want);
+    want.o = o;
+    want.disc = disc;
+    want.Wd = b->Wd;
+    for (int i = 0; i < b->rb_desc_n; ++i)
+        if (!std::memcmp(&b->rb_desc_host[i], &want, sizeof want)) return b->rb_desc_dev + i;
+    if (b->rb_desc_n >= kSlots) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(b->stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    const int i = b->rb_desc_n;
+    b->rb_desc_host[i] = want;
+    if (hipMemcpyAsync(b->rb_desc_dev + i, &b->rb_desc_host[i], sizeof(RbDesc), hipMemcpyHostToDevice, b->stream) !=
+        hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    b->rb_desc_n = i + 1;
+    return b->rb_desc_dev + i;
+}
+
+// Packed readback computed on the device (stream-ordered, no synchronisation).
+int readback_dev(mz_batch *b, float disc) {
+    int rc = flush_pending(b);
+    if (rc) return rc;
+    if (b->rb_dev_valid && b->rb_disc == disc) return MZ_OK;
+    const RbPtrs o = packed_rb(b);
     b->dirty = true;
     hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, disc, b->Wd, o);
     HIP_TRY(hipGetLastError());
@@ -6111,6 +6219,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE"))
         b->tree_nc = b->nc;
     b->zc = !getenv_flag("MZ_HOST_COPY");
+    b->fused_rb = !getenv_flag("MZ_NO_FUSED_READBACK");
     Dev &d = b->dev;
     const size_t nodes = (size_t)B * b->P;
     int rc = 0;
@@ -6144,6 +6253,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         b->rb_words = (size_t)2 * B + 2 * (size_t)B * N * A + (size_t)MZ_F_COUNT * B * b->Wd * N;
         if (N > 1) plan.dev<unsigned char>(d.o_J, (size_t)B * g.JP);
         plan.ptr(&b->rb_dev, b->rb_words);
+        plan.ptr(&b->rb_desc_dev, sizeof(b->rb_desc_host) / sizeof(RbDesc));
         rc = plan.allocate(b, d);
         if (!rc) {
             Dev chk = d;
@@ -6583,6 +6693,66 @@ int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out)
     return MZ_OK;
 }
 
+// include/mzdriver.h
+int mz_expand_backup_readback(mz_batch *b, int hsx, float discount, int K, const float *rewards, const float *values,
+                              const float *policy, const float *beta, float readback_discount,
+                              const mz_readback_out *out) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
+    if (!b->prepared) return fail(MZ_ERR_RUNTIME, "batch_expansion_and_backup before prepare");
+    if (K < 1 || K > b->K) return fail(MZ_ERR_UNSUPPORTED, "sampled_times must be in [1, the constructor's value]");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
+    RbPtrs o;
+    if (out) {
+        o.values = out->values;
+        o.mv = out->marginal_visit_count;
+        o.mp = out->marginal_priors;
+        o.deg = out->degrees;
+        for (int f = 0; f < MZ_F_COUNT; ++f) o.f[f] = (int *)out->sampled[f];
+    } else {
+        o = packed_rb(b);
+    }
+    StepArgs a{};
+    a.hsx = hsx;
+    a.discount = discount;
+    a.K = K;
+    rc = expand_inputs(b, rewards, values, policy, beta, a);
+    if (rc) return rc;
+    // the chain and tree kernels write the readback themselves (their SEL = false launches take the
+    // descriptor in the gather_out slot); the other kernels are followed by k_readback
+    const bool fusable = b->fused_rb && (b->chain3_nc > 0 || b->tree_nc > 0);
+    const RbDesc *slot = fusable ? rb_desc_slot(b, o, readback_discount) : nullptr;
+    a.gather_out = (char *)slot;
+    rc = launch_step(b, true, false, a);
+    if (rc) return rc;
+    if (!slot) {
+        b->dirty = true;
+        hipLaunchKernelGGL(k_readback, dim3(b->B), dim3(kWave), 0, b->stream, b->prm, readback_discount, b->Wd, o);
+        HIP_TRY(hipGetLastError());
+    }
+    if (!out) {  // the packed buffer now mirrors the trees
+        b->rb_dev_valid = true;
+        b->rb_valid = false;
+        b->rb_disc = readback_discount;
+    }
+    return MZ_OK;
+}
+
+int mz_readback_ready(mz_batch *b, float discount) {
+    if (!b) return fail(MZ_ERR_ARG, "null handle");
+    OrderMark om{b};
+    int rc = flush_pending(b);
+    if (rc) return rc;
+    b->prepared = true;
+    b->rb_valid = false;
+    b->rb_dev_valid = true;
+    b->rb_disc = discount;
+    return MZ_OK;
+}
+
 int mz_get_roots_values(mz_batch *b, float *out, int mem) {
     if (!b) return fail(MZ_ERR_ARG, "null handle");
     OrderMark om{b};
@@ -6595,7 +6765,7 @@ int mz_get_roots_values(mz_batch *b, float *out, int mem) {
         if (rc) return rc;
         return MZ_OK;
     }
-    rc = readback(b, b->rb_valid ? b->rb_disc : 0.f);
+    rc = readback(b, (b->rb_valid || b->rb_dev_valid) ? b->rb_disc : 0.f);
     if (rc) return rc;
     std::memcpy(out, b->rb_host, 4 * (size_t)b->B);
     return MZ_OK;
@@ -6607,7 +6777,7 @@ int mz_get_roots_marginal_visit_count(mz_batch *b, int32_t *out, int mem) {
     int rc = ensure_device(b);
     if (rc) return rc;
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
-                                : readback(b, b->rb_valid ? b->rb_disc : 0.f);
+                                : readback(b, (b->rb_valid || b->rb_dev_valid) ? b->rb_disc : 0.f);
     if (rc) return rc;
     const size_t n = (size_t)b->B * b->NA;
     if (mem == MZ_MEM_DEVICE) {
@@ -6625,7 +6795,7 @@ int mz_get_roots_marginal_priors(mz_batch *b, float *out, int mem) {
     int rc = ensure_device(b);
     if (rc) return rc;
     rc = (mem == MZ_MEM_DEVICE) ? readback_dev(b, b->rb_dev_valid ? b->rb_disc : 0.f)
-                                : readback(b, b->rb_valid ? b->rb_disc : 0.f);
+                                : readback(b, (b->rb_valid || b->rb_dev_valid) ? b->rb_disc : 0.f);
     if (rc) return rc;
     const size_t n = (size_t)b->B * b->NA;
     if (mem == MZ_MEM_DEVICE) {
@@ -6642,7 +6812,7 @@ int mz_get_num_children_of_root(mz_batch *b, int tree_id, int32_t *out) {
     if (tree_id < 0 || tree_id >= b->B) return fail(MZ_ERR_ARG, "tree_id out of range");
     int rc = ensure_device(b);
     if (rc) return rc;
-    rc = readback(b, b->rb_valid ? b->rb_disc : 0.f);
+    rc = readback(b, (b->rb_valid || b->rb_dev_valid) ? b->rb_disc : 0.f);
     if (rc) return rc;
     *out = b->rb_host[rb_deg_base(b) + tree_id];
     return MZ_OK;
@@ -6660,7 +6830,7 @@ int mz_get_root_sampled(mz_batch *b, int field, int tree_id, float discount, voi
     if (field < 0 || field >= MZ_F_COUNT) return fail(MZ_ERR_ARG, "unknown field");
     int rc = ensure_device(b);
     if (rc) return rc;
-    rc = readback(b, field == MZ_F_QVALUES ? discount : (b->rb_valid ? b->rb_disc : discount));
+    rc = readback(b, field == MZ_F_QVALUES ? discount : ((b->rb_valid || b->rb_dev_valid) ? b->rb_disc : discount));
     if (rc) return rc;
     const int deg = b->rb_host[rb_deg_base(b) + tree_id];
     const size_t per = (field == MZ_F_ACTIONS) ? (size_t)b->N : 1;

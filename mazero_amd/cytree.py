@@ -292,11 +292,8 @@ class Tree_batch:
                                                                  MZ_MEM_DEVICE), "marginal_priors_device")
         return visit_out, prior_out
 
-    def get_roots_device(self, discount: float = 0.0, values=None, marginal_visit_count=None, marginal_priors=None,
-                         degrees=None, sampled=None):
-        """Every requested readback of all roots in ONE launch, written into the given device tensors
-        (include/mzmcts.h mz_get_roots_device): values [B] f32, marginal_* [B, N, A], degrees [B] int32,
-        sampled {field name: [B, max_children(*N)]} as get_roots_sampled_padded_device lays them out."""
+    def _readback_out(self, values, marginal_visit_count, marginal_priors, degrees, sampled, what):
+        """The mz_readback_out list of caller-provided device tensors (checked: see _check_out)."""
         B, NA = self.root_num, self.agent_num * self.action_space_size
         W = self.max_children() if sampled else 0
         dv = self.device_index
@@ -310,12 +307,43 @@ class Tree_batch:
         o.marginal_priors, o.degrees = ptr(marginal_priors), ptr(degrees)
         for name, t in (sampled or {}).items():
             if name not in FIELDS:
-                raise ValueError(f"get_roots_device: unknown sampled field {name!r}")
+                raise ValueError(f"{what}: unknown sampled field {name!r}")
             width = W * self.agent_num if name == "actions" else W
             _check_out(t, B * width, torch.int32 if name in INT_FIELDS else torch.float32, f"sampled[{name!r}]", dv)
             o.sampled[FIELDS[name]] = t.data_ptr()
+        return o
+
+    def get_roots_device(self, discount: float = 0.0, values=None, marginal_visit_count=None, marginal_priors=None,
+                         degrees=None, sampled=None):
+        """Every requested readback of all roots in ONE launch, written into the given device tensors
+        (include/mzmcts.h mz_get_roots_device): values [B] f32, marginal_* [B, N, A], degrees [B] int32,
+        sampled {field name: [B, max_children(*N)]} as get_roots_sampled_padded_device lays them out."""
+        o = self._readback_out(values, marginal_visit_count, marginal_priors, degrees, sampled, "get_roots_device")
         self._sync_stream()
         check(self._lib, self._lib.mz_get_roots_device(self._h, float(discount), C.byref(o)), "get_roots_device")
+
+    def expansion_backup_readback_device(self, hidden_state_index_x, discount, sampled_times, rewards, values,
+                                         policy_probs, beta, readback_discount: float = 0.0, out: dict = None):
+        """The search's last batch_expansion_and_backup (device inputs) and the readback of every root
+        output in one launch (include/mzdriver.h mz_expand_backup_readback).  `out`: get_roots_device's
+        keyword arguments (values, marginal_visit_count, marginal_priors, degrees, sampled) as a dict;
+        None writes the handle's packed readback buffer instead, which the host getters then copy."""
+        ts = [_f32_dev(t) for t in (rewards, values, policy_probs, beta)]
+        o = None
+        if out is not None:
+            o = self._readback_out(out.get("values"), out.get("marginal_visit_count"), out.get("marginal_priors"),
+                                   out.get("degrees"), out.get("sampled"), "expansion_backup_readback_device")
+        self._sync_stream()
+        rc = self._lib.mz_expand_backup_readback(
+            self._h, int(hidden_state_index_x), float(discount), int(sampled_times),
+            *[C.c_void_p(t.data_ptr()) for t in ts], float(readback_discount), None if o is None else C.byref(o))
+        check(self._lib, rc, "expansion_backup_readback_device")
+
+    def readback_ready(self, discount: float):
+        """After replaying a graph that ended with expansion_backup_readback_device(packed=True): the
+        packed readback is current for `discount` (include/mzdriver.h mz_readback_ready)."""
+        self._sync_stream()
+        check(self._lib, self._lib.mz_readback_ready(self._h, float(discount)), "readback_ready")
 
     def get_roots_sampled_padded_device(self, name: str, discount: float = 0.0, degrees_out=None):
         """Device form of get_roots_sampled_padded: (tensor [B, maxdeg(*N)], degrees int32 [B])."""

@@ -149,6 +149,7 @@ class _SearchLoop:
         self.graph_nodes = None  # (nodes, memset nodes) of the recorded graph
         self.runs = 0
         self.storage = None  # _storage_signature(model) when the loop was made
+        self.fused_rb = hasattr(tb._lib, "mz_expand_backup_readback")
 
     def load(self, hidden, root_arrays, factor):
         self.root.copy_(hidden.reshape(self.B, -1))
@@ -248,6 +249,11 @@ class _SearchLoop:
                                                      out=self.sel, pool=None if chain else self.pool,
                                                      gather_out=None if chain else self.leaf)
                 leaf = nh if chain else self.leaf
+            elif self.fused_rb:
+                # the last expansion also writes the packed readback (mz_expand_backup_readback): the
+                # SearchOutput getters then only copy it to the host
+                tb.expansion_backup_readback_device(s + 1, disc, K, r32, v32, self.probs, self.beta,
+                                                    readback_discount=disc)
             else:
                 tb.batch_expansion_and_backup(s + 1, disc, K, r32, v32, self.probs, self.beta)
 
@@ -499,7 +505,10 @@ class SampledMCTS:
                     st.capture(model, cfg, eps, sampled_tau)  # (records only: nothing runs)
                 if self.use_graph and st.runs > 0 and st.graph:
                     st.graph.replay()
-                    tb.state_changed()
+                    if st.fused_rb:  # (its last launch left the packed readback)
+                        tb.readback_ready(disc)
+                    else:
+                        tb.state_changed()
                 else:
                     st.run(model, cfg, eps, sampled_tau)  # eager (the first search also warms up)
                 st.runs += 1

@@ -51,9 +51,12 @@ def to_device(inp):
                    value=f(inp.value), policy=f(inp.policy), beta=f(inp.beta))
 
 
-def run_fused(tb, dinp, K, knobs, pool=None):
+def run_fused(tb, dinp, K, knobs, pool=None, fused_rb=None):
     """The device-resident loop: prepare, select(0), then per simulation one fused
-    expand+backup+select(+gather) launch; selections are recorded on the device."""
+    expand+backup+select(+gather) launch; selections are recorded on the device.  fused_rb: None,
+    the last expansion alone (then the host getters); "packed", the last expansion fused with the
+    packed readback (mz_expand_backup_readback, out = NULL) before the host getters; a dict of
+    get_roots_device output tensors, fused with the readback into them."""
     from mazero_amd.synthetic import DEFAULTS, readbacks
 
     k = dict(DEFAULTS)
@@ -78,6 +81,10 @@ def run_fused(tb, dinp, K, knobs, pool=None):
             tb.expansion_backup_selection_device(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s],
                                                  dinp.beta[s], c2, c1, out=(idx[s + 1], idy[s + 1], act[s + 1]),
                                                  pool=pool, gather_out=None if pool is None else gathered[s + 1])
+        elif fused_rb is not None:
+            tb.expansion_backup_readback_device(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s],
+                                                dinp.beta[s], readback_discount=g,
+                                                out=None if fused_rb == "packed" else fused_rb)
         else:
             tb.batch_expansion_and_backup(s + 1, g, K, dinp.reward[s], dinp.value[s], dinp.policy[s], dinp.beta[s])
     torch.cuda.synchronize()
@@ -234,6 +241,64 @@ def test_seeding_paths_vs_port(gpu_lib, port_lib, seeding, K, monkeypatch):
     out, _ = run_fused(tb, to_device(inp), K, {})
     exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
     assert_same(out, exp, f"gpu seeding={seeding} K={K} ")
+
+
+FUSED_RB = [
+    # (name, B, A, K, S, env): which kernel ends the search -- k_chain3 / k_tree write the readback
+    # themselves, the others are followed by k_readback; S = 1: the last leaf is a root child
+    ("chain3", 64, 9, 1, 30, None), ("chain3_s1", 64, 9, 1, 1, None), ("tree", 64, 9, 5, 30, None),
+    ("tree_s1", 64, 9, 5, 1, None), ("tree_k10", 32, 15, 10, 40, None), ("chain_v2", 64, 9, 1, 30, "MZ_CHAIN_V2"),
+    ("kstep_k70", 16, 64, 70, 12, None), ("chain512", 16, 9, 1, 300, None),
+    ("unfused_env", 64, 9, 5, 30, "MZ_NO_FUSED_READBACK"),
+]
+
+
+@pytest.mark.parametrize("name,B,A,K,S,env", FUSED_RB, ids=[f[0] for f in FUSED_RB])
+def test_fused_readback(gpu_lib, port_lib, name, B, A, K, S, env, monkeypatch):
+    """mz_expand_backup_readback: the search's last expansion with every root output, into the
+    packed buffer (then the host getters, against the CPU port) and into caller tensors (against
+    mz_get_roots_device on the same final state), for every kernel that can end a search."""
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    rng = np.random.default_rng(sum(map(ord, name)) + 31 * S)
+    inp = make_search_inputs(rng, B, A, S, legal_zero_frac=0.2)
+    exp = run_search(make_tb(port_lib, inp, K, {}), inp, K, {})
+    exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    if env:
+        monkeypatch.setenv(env, "1")
+    tb = make_tb(gpu_lib, inp, K, {})
+    tb2 = make_tb(gpu_lib, inp, K, {})
+    if env:
+        monkeypatch.delenv(env)
+    out, _ = run_fused(tb, to_device(inp), K, {}, fused_rb="packed")
+    assert_same(out, exp, f"gpu fused packed readback {name} ")
+    # into caller tensors: every field, against a separate readback of the same final state
+    dev = torch.device("cuda")
+    NA = A
+    W = min(K, A)
+    from mazero_amd._capi import FIELDS, INT_FIELDS
+
+    def outs():
+        return dict(values=torch.full((B,), -7.0, device=dev),
+                    marginal_visit_count=torch.full((B, 1, NA), -7, dtype=torch.int32, device=dev),
+                    marginal_priors=torch.full((B, 1, NA), -7.0, device=dev),
+                    degrees=torch.full((B,), -7, dtype=torch.int32, device=dev),
+                    sampled={f: torch.full((B, W), -7, dtype=torch.int32 if f in INT_FIELDS else torch.float32,
+                                           device=dev) for f in FIELDS})
+    got = outs()
+    run_fused(tb2, to_device(inp), K, {}, fused_rb=got)
+    ref = outs()
+    from mazero_amd.synthetic import DEFAULTS
+
+    tb2.get_roots_device(DEFAULTS["discount"], **ref)
+    torch.cuda.synchronize()
+    for k in ("values", "marginal_visit_count", "marginal_priors", "degrees"):
+        assert torch.equal(got[k].view(torch.int32) if got[k].is_floating_point() else got[k],
+                           ref[k].view(torch.int32) if ref[k].is_floating_point() else ref[k]), (name, k)
+    for f in FIELDS:
+        a, b = got["sampled"][f], ref["sampled"][f]
+        assert torch.equal(a.view(torch.int32) if a.is_floating_point() else a,
+                           b.view(torch.int32) if b.is_floating_point() else b), (name, f)
 
 
 def test_chain_v2_on_reference_fixture(gpu_lib, monkeypatch):
