@@ -42,7 +42,10 @@ for c in $CONFIGS; do
     cpu="--no-cpu"; [ "$c" = 3m_k1 ] && cpu=""
     # (27m: 27 agent searches x 200 sims = 5,400 fused dispatches per env step; rocprofv3's PMC
     # collection crashed on the host at --steps 3, so those passes profile one step)
-    ps="--steps 3 --warmup 1"; case $c in 27m*) ps="--steps 1 --warmup 1";; esac
+    # (27m K = 1 under --pmc with the env step captured as one graph of 5,481 kernel nodes: rocprofv3
+    # segfaults a few seconds into the replay, profiles/round4/pmc_crash_27m_k1_graph.log; the 27m PMC
+    # passes launch eagerly, --no-graph, the same kernels)
+    ps="--steps 3 --warmup 1"; case $c in 27m*) ps="--steps 1 --warmup 1 --no-graph";; esac
     step "$d/pmc_fetch.json" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$d/pmc_fetch" -o run -- \
         python3 "$R/bench.py" --no-cpu $ps $a
     step "$d/pmc_write.json" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/$d/pmc_write" -o run -- \
