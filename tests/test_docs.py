@@ -3,7 +3,7 @@
 DESIGN.md / README.md / INTEGRATION.md / scripts/README.md quote numbers from `profiles/` and name
 files of this repository.  These checks keep them from drifting: every repository file they name
 exists, README's headline is the committed headline bench line, and DESIGN §5's configuration table
-is the committed reconciliation (`profiles/round3/roofline_reconcile.json`)."""
+is the committed reconciliation (`profiles/round4/roofline_reconcile.json`)."""
 from __future__ import annotations
 
 import json
@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOCS = ["DESIGN.md", "README.md", "INTEGRATION.md", os.path.join("scripts", "README.md")]
-ROUND = os.path.join(ROOT, "profiles", "round3")
+ROUND = os.path.join(ROOT, "profiles", "round4")
 
 # names of the reference's own sources (in /root/reference, cited by file:line) and of files a
 # document says are gone
@@ -41,7 +41,7 @@ def test_named_files_exist(doc):
             assert os.path.exists(os.path.join(ROUND, "3m_k1", n)), n
             continue
         cands = [n] + [os.path.join(d, n) for d in ("scripts", "mazero_amd", "mazero_amd/csrc", "oracle", "include",
-                                                     "tests", "profiles/round3", "profiles")]
+                                                     "tests", "profiles/round4", "profiles/round3", "profiles")]
         if not any(os.path.exists(os.path.join(ROOT, c)) for c in cands):
             missing.append(n)
     assert not missing, f"{doc} names files that do not exist: {missing}"
