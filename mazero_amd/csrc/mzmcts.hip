@@ -163,6 +163,9 @@ struct Params {
     // null: k_prepare runs the seeding chain
     const unsigned *cp;
     unsigned cp_n;
+    // the host-path stage's error word (device mapping of pinned host memory), or null: kernels OR
+    // every error into it too, so a host-path call learns its errors without a copy launch
+    int *herr;
 };
 
 // Arena offsets of every array a k_step launch reads in its first round, as a function of the
@@ -206,6 +209,14 @@ __host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned 
     d.o_sq = o; o += span_n<8>(PS + kWave);
     d.o_path = o; o += span_n<8>(B * PS);
     d.o_V = o;  // [P][E] value entries, E = S + 1 = PS - 1
+}
+
+// Report error bits: the handle's device error word and, when the host path's stage exists, its
+// mirror in pinned host memory (Params::herr; system scope, rare: only trees that fail)
+__device__ __forceinline__ void raise_err(const Dev &d, int e) {
+    atomicOr(d.err(), e);
+    int *h = ((const Params *)(const void *)d.base)->herr;
+    if (h) __hip_atomic_fetch_or(h, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #ifdef MZ_ARGCHECK
@@ -992,7 +1003,10 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     // the handle's error word starts clean (no runtime memset node in captured graphs).  A tree's
     // error also stays in its header, and every later kernel re-reports the errors of dead trees,
     // so an error raised by another block before this store is not lost.
-    if (t == 0 && tid == 0) *d.err() = 0;
+    if (t == 0 && tid == 0) {
+        *d.err() = 0;
+        if (prm->herr) __hip_atomic_store(prm->herr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     const unsigned seed_v = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
     const unsigned *cp = prm->cp;
     if (cp && seed_v < prm->cp_n) {
@@ -1183,7 +1197,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
                 st[MZ_S_PATH_EDGES] += 1;
             }
         }
-        if (err) atomicOr(d.err(), err);
+        if (err) raise_err(d, err);
     }
 }
 
@@ -2250,7 +2264,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
     }
 #endif
     if (h.err) {  // a dead tree stays dead (both waves see the same header) and re-reports its error
-        if (wv == 0 && l == 0) atomicOr(d.err(), h.err);
+        if (wv == 0 && l == 0) raise_err(d, h.err);
         if (SEL && wv == 0) {
             if (l == 0) {
                 a.idx_x[t] = 0;
@@ -2552,7 +2566,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
     }
     wait_lds();
     if (l < kStatN) st[l] = st_old + xst[l] + (EB ? xst[MZ_S_COUNT + l] : 0ll);
-    if (l == 0 && err) atomicOr(d.err(), err);
+    if (l == 0 && err) raise_err(d, err);
 #ifdef MZ_ARGCHECK
     if (l == 0 && err)
         argcheck_record(2 + wv, EB, SEL, t, base, P, PS, BA, pk, K, hsx, discount, pe, ne, d.hdr() + t, h.tot,
@@ -2868,7 +2882,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
                     idy[t] = t;
                     act[t] = 0;
                 }
-                atomicOr(d.err(), h.err);
+                raise_err(d, h.err);
             }
         }
         wait_vm();  // (the row's loads / chunks)
@@ -2886,7 +2900,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
                 }
                 TreeHdr *hp = d.hdr() + t;
                 hp->err = kErrPath;
-                atomicOr(d.err(), kErrPath);
+                raise_err(d, kErrPath);
             }
             wait_vm();
             return;
@@ -3130,7 +3144,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
         }
         st[l] = (long long)st_old + add;
     }
-    if (l == 0 && err) atomicOr(d.err(), err);
+    if (l == 0 && err) raise_err(d, err);
     span_close(hsx, rt0);
 }
 
@@ -3555,7 +3569,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                 idy[t] = t;
                 act[t] = 0;
             }
-            atomicOr(d.err(), h.err);
+            raise_err(d, h.err);
         }
         return;
     }
@@ -3569,7 +3583,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                     act[t] = 0;
                 }
                 hp->err = kErrPath;
-                atomicOr(d.err(), kErrPath);
+                raise_err(d, kErrPath);
             }
             return;
         }
@@ -3732,7 +3746,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                              l == MZ_S_CYC_W1_STAGE2;
         if (!w2_slot) st[l] += add;
     }
-    if (l == 0 && err) atomicOr(d.err(), err);
+    if (l == 0 && err) raise_err(d, err);
     span_close(hsx, rt0);
 }
 
@@ -4858,7 +4872,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 idy[t] = t;
                 act[t] = 0;
             }
-            atomicOr(d.err(), h.err);
+            raise_err(d, h.err);
         }
         wait_vm();
         return;
@@ -5307,7 +5321,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         }
         st[l] = st_old + add;
     }
-    if (l == 0 && err) atomicOr(d.err(), err);
+    if (l == 0 && err) raise_err(d, err);
     span_close(hsx, rt0);
     span_info(hsx, (unsigned long long)(D & 0xffff) | ((unsigned long long)(ntot & 0xffff) << 16) |
                        ((unsigned long long)(Dn & 0xffff) << 32), rt0, rm1, rm2, rm3);
@@ -5352,7 +5366,7 @@ __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm,
     const int fc = uni(rbn.x);
     {
         const int herr = d.hdr()[t].err;  // dead trees re-report their error (see k_prepare)
-        if (l == 0 && herr) atomicOr(d.err(), herr);
+        if (l == 0 && herr) raise_err(d, herr);
     }
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
     float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -5416,6 +5430,9 @@ struct mz_batch {
     float *st_in = nullptr;
     int32_t *st_sel = nullptr;
     int32_t *st_err = nullptr;
+    int *herr_dev = nullptr;    // st_err's device mapping, the source of Params::herr's upload
+    bool herr_pending = false;  // Params::herr set on the stream; live after the next check
+    bool herr_live = false;     // every kernel mirrors its errors into st_err: checks need no copy
     // zero-copy (default; MZ_HOST_COPY=1 at mz_create: DMA copies instead): the kernels read the
     // staged inputs and write the selection straight through the stage's device mapping
     bool zc = true;
@@ -5562,16 +5579,24 @@ int copy_words(mz_batch *b, void *dst, const int *src, size_t n);
 int check_device_errors(mz_batch *b) {
     int rc = ensure_stage(b);
     if (rc) return rc;
-    if (b->zc) {  // (a one-word kernel store into the stage's device mapping: no DMA round trip)
-        rc = copy_words(b, b->st_err_d, b->dev.err(), 1);
-        if (rc) return rc;
-    } else {
-        HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
+    // Once the kernels mirror their errors into the stage (Params::herr), the stage's word equals
+    // the device word (both ORed by every report, both cleared by k_prepare): no copy launch
+    if (!b->herr_live) {
+        if (b->zc) {  // (a one-word kernel store into the stage's device mapping: no DMA round trip)
+            rc = copy_words(b, b->st_err_d, b->dev.err(), 1);
+            if (rc) return rc;
+        } else {
+            HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
+        }
     }
     HIP_TRY(hipStreamSynchronize(b->stream));
+    if (b->herr_pending) {  // (the copy above, after the Params update, started the mirror equal)
+        b->herr_pending = false;
+        b->herr_live = true;
+    }
     b->st_busy = false;  // (every copy out of the stage has completed)
     b->dirty = b->order_live = false;  // nothing of this handle is in flight
-    const int e = *b->st_err;
+    const int e = *(volatile int32_t *)b->st_err;
     if (e) {
         char bits[32];
         std::snprintf(bits, sizeof bits, " (device error word 0x%x)", (unsigned)e);
@@ -5911,6 +5936,18 @@ int ensure_stage(mz_batch *b) {
     b->st_in_d = (const float *)pd;
     b->st_sel_d = (int32_t *)pd + w_in;
     b->st_err_d = (int32_t *)pd + w_in + w_sel;
+    *b->st_err = 0;
+    if (b->zc) {  // the kernels mirror their errors into the stage from the next launch on
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(b->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+            b->herr_dev = b->st_err_d;
+            HIP_TRY(hipMemcpyAsync((char *)b->prm + offsetof(Params, herr), &b->herr_dev, sizeof(int *),
+                                   hipMemcpyHostToDevice, b->stream));
+            b->herr_pending = true;
+        } else {
+            (void)hipGetLastError();
+        }
+    }
     return MZ_OK;
 }
 
