@@ -32,6 +32,7 @@
 // operations, so no device transcendental enters a result.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -163,9 +164,6 @@ struct Params {
     // null: k_prepare runs the seeding chain
     const unsigned *cp;
     unsigned cp_n;
-    // the host-path stage's error word (device mapping of pinned host memory), or null: kernels OR
-    // every error into it too, so a host-path call learns its errors without a copy launch
-    int *herr;
 };
 
 // Arena offsets of every array a k_step launch reads in its first round, as a function of the
@@ -209,14 +207,6 @@ __host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned 
     d.o_sq = o; o += span_n<8>(PS + kWave);
     d.o_path = o; o += span_n<8>(B * PS);
     d.o_V = o;  // [P][E] value entries, E = S + 1 = PS - 1
-}
-
-// Report error bits: the handle's device error word and, when the host path's stage exists, its
-// mirror in pinned host memory (Params::herr; system scope, rare: only trees that fail)
-__device__ __forceinline__ void raise_err(const Dev &d, int e) {
-    atomicOr(d.err(), e);
-    int *h = ((const Params *)(const void *)d.base)->herr;
-    if (h) __hip_atomic_fetch_or(h, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #ifdef MZ_ARGCHECK
@@ -1003,10 +993,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
     // the handle's error word starts clean (no runtime memset node in captured graphs).  A tree's
     // error also stays in its header, and every later kernel re-reports the errors of dead trees,
     // so an error raised by another block before this store is not lost.
-    if (t == 0 && tid == 0) {
-        *d.err() = 0;
-        if (prm->herr) __hip_atomic_store(prm->herr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (t == 0 && tid == 0) *d.err() = 0;
     const unsigned seed_v = d.seed()[0] * 2333u + (unsigned)(g.root_offset + t);
     const unsigned *cp = prm->cp;
     if (cp && seed_v < prm->cp_n) {
@@ -1197,7 +1184,7 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
                 st[MZ_S_PATH_EDGES] += 1;
             }
         }
-        if (err) raise_err(d, err);
+        if (err) atomicOr(d.err(), err);
     }
 }
 
@@ -2264,7 +2251,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
     }
 #endif
     if (h.err) {  // a dead tree stays dead (both waves see the same header) and re-reports its error
-        if (wv == 0 && l == 0) raise_err(d, h.err);
+        if (wv == 0 && l == 0) atomicOr(d.err(), h.err);
         if (SEL && wv == 0) {
             if (l == 0) {
                 a.idx_x[t] = 0;
@@ -2566,7 +2553,7 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
     }
     wait_lds();
     if (l < kStatN) st[l] = st_old + xst[l] + (EB ? xst[MZ_S_COUNT + l] : 0ll);
-    if (l == 0 && err) raise_err(d, err);
+    if (l == 0 && err) atomicOr(d.err(), err);
 #ifdef MZ_ARGCHECK
     if (l == 0 && err)
         argcheck_record(2 + wv, EB, SEL, t, base, P, PS, BA, pk, K, hsx, discount, pe, ne, d.hdr() + t, h.tot,
@@ -2882,7 +2869,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
                     idy[t] = t;
                     act[t] = 0;
                 }
-                raise_err(d, h.err);
+                atomicOr(d.err(), h.err);
             }
         }
         wait_vm();  // (the row's loads / chunks)
@@ -2900,7 +2887,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
                 }
                 TreeHdr *hp = d.hdr() + t;
                 hp->err = kErrPath;
-                raise_err(d, kErrPath);
+                atomicOr(d.err(), kErrPath);
             }
             wait_vm();
             return;
@@ -3144,7 +3131,7 @@ __global__ __launch_bounds__(128) void k_chain(char *base, const float *policy, 
         }
         st[l] = (long long)st_old + add;
     }
-    if (l == 0 && err) raise_err(d, err);
+    if (l == 0 && err) atomicOr(d.err(), err);
     span_close(hsx, rt0);
 }
 
@@ -3569,7 +3556,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                 idy[t] = t;
                 act[t] = 0;
             }
-            raise_err(d, h.err);
+            atomicOr(d.err(), h.err);
         }
         return;
     }
@@ -3583,7 +3570,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                     act[t] = 0;
                 }
                 hp->err = kErrPath;
-                raise_err(d, kErrPath);
+                atomicOr(d.err(), kErrPath);
             }
             return;
         }
@@ -3746,7 +3733,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                              l == MZ_S_CYC_W1_STAGE2;
         if (!w2_slot) st[l] += add;
     }
-    if (l == 0 && err) raise_err(d, err);
+    if (l == 0 && err) atomicOr(d.err(), err);
     span_close(hsx, rt0);
 }
 
@@ -4872,7 +4859,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 idy[t] = t;
                 act[t] = 0;
             }
-            raise_err(d, h.err);
+            atomicOr(d.err(), h.err);
         }
         wait_vm();
         return;
@@ -5321,10 +5308,35 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         }
         st[l] = st_old + add;
     }
-    if (l == 0 && err) raise_err(d, err);
+    if (l == 0 && err) atomicOr(d.err(), err);
     span_close(hsx, rt0);
     span_info(hsx, (unsigned long long)(D & 0xffff) | ((unsigned long long)(ntot & 0xffff) << 16) |
                        ((unsigned long long)(Dn & 0xffff) << 32), rt0, rm1, rm2, rm3);
+}
+
+// mz_create's device initialisation in one launch (instead of three copies and three memsets,
+// each a synchronous runtime call): the Params block, the seed word, the lambda powers (the float
+// chain lp[k] = lp[k - 1] * lam of utils.cpp:25-27, on one thread, in the order the host ran it),
+// zeroed tree headers, statistics and error word
+__global__ __launch_bounds__(256) void k_init(Params p, unsigned seed, float lam, int nlp, int hdr_words,
+                                              int stat_words) {
+    const Dev &d = p.d;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        *(Params *)(void *)d.base = p;
+        *d.seed() = seed;
+        *d.err() = 0;
+        float *lp = d.lp();
+        float v = 1.0f;
+        lp[0] = v;
+        for (int k = 1; k < p.g.PS + 1; ++k) {
+            v = v * lam;
+            lp[k] = v;
+        }
+        for (int k = p.g.PS + 1; k < nlp; ++k) lp[k] = 0.f;
+    }
+    for (int w = i; w < hdr_words; w += gridDim.x * 256) ((int *)d.hdr())[w] = 0;
+    for (int w = i; w < stat_words; w += gridDim.x * 256) ((int *)d.stats())[w] = 0;
 }
 
 // Standalone hidden-state gather: out[i] = pool[idx_x[i]][i]   (mcts_sampled.py:130-134)
@@ -5366,7 +5378,7 @@ __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm,
     const int fc = uni(rbn.x);
     {
         const int herr = d.hdr()[t].err;  // dead trees re-report their error (see k_prepare)
-        if (l == 0 && herr) raise_err(d, herr);
+        if (l == 0 && herr) atomicOr(d.err(), herr);
     }
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
     float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -5430,9 +5442,6 @@ struct mz_batch {
     float *st_in = nullptr;
     int32_t *st_sel = nullptr;
     int32_t *st_err = nullptr;
-    int *herr_dev = nullptr;    // st_err's device mapping, the source of Params::herr's upload
-    bool herr_pending = false;  // Params::herr set on the stream; live after the next check
-    bool herr_live = false;     // every kernel mirrors its errors into st_err: checks need no copy
     // zero-copy (default; MZ_HOST_COPY=1 at mz_create: DMA copies instead): the kernels read the
     // staged inputs and write the selection straight through the stage's device mapping
     bool zc = true;
@@ -5508,6 +5517,19 @@ void seed_table(int dev, unsigned long long need, const unsigned **cp, unsigned 
     *cp_n = st.n;
 }
 
+// A non-blocking stream per device for mz_create's initialisation launch (never captured, so a
+// capture running on another stream is not disturbed)
+hipStream_t init_stream(int dev) {
+    static hipStream_t st[kSeedTabDevices];
+    if (dev < 0 || dev >= kSeedTabDevices) return nullptr;
+    std::lock_guard<std::mutex> lk(g_seed_mu);
+    if (!st[dev] && hipStreamCreateWithFlags(&st[dev], hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        st[dev] = nullptr;
+    }
+    return st[dev];
+}
+
 bool getenv_flag(const char *name) {
     const char *v = std::getenv(name);
     return v && v[0] == '1';
@@ -5579,24 +5601,16 @@ int copy_words(mz_batch *b, void *dst, const int *src, size_t n);
 int check_device_errors(mz_batch *b) {
     int rc = ensure_stage(b);
     if (rc) return rc;
-    // Once the kernels mirror their errors into the stage (Params::herr), the stage's word equals
-    // the device word (both ORed by every report, both cleared by k_prepare): no copy launch
-    if (!b->herr_live) {
-        if (b->zc) {  // (a one-word kernel store into the stage's device mapping: no DMA round trip)
-            rc = copy_words(b, b->st_err_d, b->dev.err(), 1);
-            if (rc) return rc;
-        } else {
-            HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
-        }
+    if (b->zc) {  // (a one-word kernel store into the stage's device mapping: no DMA round trip)
+        rc = copy_words(b, b->st_err_d, b->dev.err(), 1);
+        if (rc) return rc;
+    } else {
+        HIP_TRY(hipMemcpyAsync(b->st_err, b->dev.err(), sizeof(int), hipMemcpyDeviceToHost, b->stream));
     }
     HIP_TRY(hipStreamSynchronize(b->stream));
-    if (b->herr_pending) {  // (the copy above, after the Params update, started the mirror equal)
-        b->herr_pending = false;
-        b->herr_live = true;
-    }
     b->st_busy = false;  // (every copy out of the stage has completed)
     b->dirty = b->order_live = false;  // nothing of this handle is in flight
-    const int e = *(volatile int32_t *)b->st_err;
+    const int e = *b->st_err;
     if (e) {
         char bits[32];
         std::snprintf(bits, sizeof bits, " (device error word 0x%x)", (unsigned)e);
@@ -5936,18 +5950,6 @@ int ensure_stage(mz_batch *b) {
     b->st_in_d = (const float *)pd;
     b->st_sel_d = (int32_t *)pd + w_in;
     b->st_err_d = (int32_t *)pd + w_in + w_sel;
-    *b->st_err = 0;
-    if (b->zc) {  // the kernels mirror their errors into the stage from the next launch on
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(b->stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
-            b->herr_dev = b->st_err_d;
-            HIP_TRY(hipMemcpyAsync((char *)b->prm + offsetof(Params, herr), &b->herr_dev, sizeof(int *),
-                                   hipMemcpyHostToDevice, b->stream));
-            b->herr_pending = true;
-        } else {
-            (void)hipGetLastError();
-        }
-    }
     return MZ_OK;
 }
 
@@ -6319,17 +6321,17 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         seed_table(b->device, 255ull * 2333ull + (unsigned long long)(root_offset > 0 ? root_offset : 0) + (unsigned long long)B,
                    &seed_cp, &seed_cp_n);
     const Params host_params{b->geo, b->dev, seed_cp, seed_cp_n};
-    std::vector<float> lp(b->PS + 1 + kWave, 0.f);
-    lp[0] = 1.0f;
-    for (int k = 1; k < b->PS + 1; ++k) lp[k] = lp[k - 1] * lam;  // lam_pow chain (utils.cpp:25-27)
-    if (hipMemcpy(d.lp(), lp.data(), sizeof(float) * lp.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d.seed(), &seed, sizeof(unsigned), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(b->prm, &host_params, sizeof(Params), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(d.hdr(), 0, sizeof(TreeHdr) * B) != hipSuccess ||
-        hipMemset(d.stats(), 0, sizeof(long long) * B * MZ_S_COUNT) != hipSuccess ||
-        hipMemset(d.err(), 0, sizeof(int)) != hipSuccess) {
-        mz_destroy(b);
-        return fail(MZ_ERR_DEVICE, "device initialisation failed");
+    {
+        // one launch on the device's init stream, waited for here (the handle's stream is bound later)
+        hipStream_t is = init_stream(b->device);
+        const int hw = (int)(sizeof(TreeHdr) / 4) * B, sw = 2 * MZ_S_COUNT * B;
+        const int nblk = (int)std::min<long long>(1024, ((long long)(hw > sw ? hw : sw) + 255) / 256 + 1);
+        hipLaunchKernelGGL(k_init, dim3(nblk), dim3(256), 0, is, host_params, seed, lam, b->PS + 1 + kWave, hw, sw);
+        if (!is || hipGetLastError() != hipSuccess || hipStreamSynchronize(is) != hipSuccess) {
+            (void)hipGetLastError();
+            mz_destroy(b);
+            return fail(MZ_ERR_DEVICE, "device initialisation failed");
+        }
     }
     if (g.lds > 64 * 1024) {
 #ifndef MZ_NO_JOINT
