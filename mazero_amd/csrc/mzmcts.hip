@@ -6186,6 +6186,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
 #ifdef MZ_NO_TABLE
     g.use_table = 0;
 #endif
+    auto lay = [&]() {
     int o = 0;
     g.oA = o; o += round16(16 * g.P);
     g.oB = o; o += round16(16 * g.P);
@@ -6218,6 +6219,17 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         g.oJ = g.oJpol = g.oJbet = g.oJcp = g.oJdraw = 0;
     }
     g.lds = o;
+    };
+    lay();
+    if (g.lds > 160 * 1024 && N == 1) {
+        // a pool too large for the LDS image as laid out: the pUCT coefficients from the pb / sq
+        // tables instead of a staged table, and smaller value-entry chunks (the back-propagation
+        // stages a path node's entries chunk by chunk), before refusing the tree (k_step's general
+        // layout: 3m-sized actions at K = 10 reach S = 200 this way)
+        g.use_table = 0;
+        if (g.reg_cap > 512) g.reg_cap = (S + 1 > 512) ? S + 1 : 512;
+        lay();
+    }
     // compile-time layout class (pb / sq pUCT tables, value-entry chunks of kRegCap)
     b->nc = 0;
     for (int nc : {64, 128, 256, 384, 512, 1024})

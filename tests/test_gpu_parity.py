@@ -184,13 +184,18 @@ BIG = [
     ("k1_chain512", 64, 9, 1, 300, 0.3),
     ("k1_chain1024", 32, 11, 1, 700, 0.0),
     ("k1_chain_general", 16, 9, 1, 1100, 0.0),
+    # pools past 1,024 nodes whose LDS image fits only without the staged pUCT table and with
+    # 512-entry value chunks (mz_create's second layout): K = 10 at S = 200
+    ("k10_s200_general", 16, 9, 10, 200, 0.3),
+    ("27m_k10_s200", 8, 36, 10, 200, 0.0),
 ]
 
 
 # the fused kernel each row exists for (mz_fused_kernel)
 BIG_KERNEL = {"3m_k1": "k_chain3<64>", "27m_k1": "k_chain3<256>", "k1_chain512": "k_chain<512>",
               "k1_chain1024": "k_chain<1024>", "k1_chain_general": "k_chain<0>",
-              "27m_k8_general_layout": "k_step<0>", "k2_long_value_sets": "k_step<1024>"}
+              "27m_k8_general_layout": "k_step<0>", "k2_long_value_sets": "k_step<1024>",
+              "k10_s200_general": "k_step<0>", "27m_k10_s200": "k_step<0>"}
 
 
 @pytest.mark.parametrize("name,B,A,K,S,lz", BIG, ids=[b[0] for b in BIG])
