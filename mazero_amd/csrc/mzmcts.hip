@@ -376,6 +376,15 @@ __device__ __forceinline__ void readback_emit(const RbPtrs &o, float disc, int W
 // Wait for this wave's memory traffic (LDS-DMA included via vmcnt) / LDS traffic; compiler fence.
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// A store with the system-coherence bits (sc0 sc1): written through to memory rather than left
+// dirty in L2, so the dependent-kernel boundary has less to write back.  Only for data this
+// kernel does not read again (the asm is invisible to the compiler's wait counting).
+__device__ __forceinline__ void st_wt16(void *p, int4 v) {
+    typedef int i4v __attribute__((ext_vector_type(4)));
+    const i4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+}
+
 // Workgroup barrier for data exchanged through LDS only: unlike __syncthreads() it does not wait for
 // the wave's outstanding global stores (vmcnt), which take ~1,000 cycles to drain.  LDS-DMA data
 // a wave hands over must be waited for (wait_vm) before it.
@@ -3469,13 +3478,18 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         if (SEL && ROW != 3 && !err) {
             char *dst = gather_out + (long long)t * row_bytes;
             if constexpr (ROW == 1) {
-                if (o < row_bytes) *(int4 *)(dst + o) = gv0;
-                if (o + 1024 < row_bytes) *(int4 *)(dst + o + 1024) = gv1;
-                if (o + 2048 < row_bytes) *(int4 *)(dst + o + 2048) = gv2;
-                if (o + 3072 < row_bytes) *(int4 *)(dst + o + 3072) = gv3;
+                // written through (sc0 sc1): the rows are most of this launch's stores, and lines
+                // left dirty in L2 are written back at the kernel boundary (same-box A/B: 3m env
+                // step 0.4743 -> 0.4679 ms, 2s3z 1.110 -> 1.080; k_tree's 3m row measured 0.5 %
+                // slower this way)
+                if (o < row_bytes) st_wt16(dst + o, gv0);
+                if (o + 1024 < row_bytes) st_wt16(dst + o + 1024, gv1);
+                if (o + 2048 < row_bytes) st_wt16(dst + o + 2048, gv2);
+                if (o + 3072 < row_bytes) st_wt16(dst + o + 3072, gv3);
             } else if constexpr (ROW == 2) {
                 wait_vm();
-                for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(dst + o2) = *(const int4 *)(sbig + o2);
+                // (written through as well: 27m's 13.5 KiB rows, env step 26.42 -> 24.53 ms)
+                for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) st_wt16(dst + o2, *(const int4 *)(sbig + o2));
             } else {  // any other row: 16-byte copies when aligned, else 4-byte
                 if (((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) & 15) == 0) {
                     for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(dst + o2) = *(const int4 *)(src + o2);
@@ -5269,7 +5283,11 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #ifdef MZ_SPANS_EPI
         rm3 = span_mark();
 #endif
+#ifdef MZ_WT_TREE_ROW  // experiment: the row written through
+        for (long long o = (long long)l * 16; o < row_bytes; o += 16 * kWave) st_wt16(gdst + o, *(const int4 *)(sbig + o));
+#else
         for (long long o = (long long)l * 16; o < row_bytes; o += 16 * kWave) *(int4 *)(gdst + o) = *(const int4 *)(sbig + o);
+#endif
     }
     stamp(ts, 8);
     if (l < kStatN) {
