@@ -713,25 +713,6 @@ def test_get_roots_device_checks_outputs(gpu_lib):
     assert np.array_equal(v.cpu().numpy().view(np.int32), tb.get_roots_values().view(np.int32))
 
 
-def _fuzz_configs(seed: int, n: int):
-    """Seeded random small configurations across the kernels' classes and the search knobs."""
-    rng = np.random.default_rng(seed)
-    out = []
-    for _ in range(n):
-        A = int(rng.choice([1, 2, 3, 5, 9, 11, 15, 16, 17, 36, 63, 64]))
-        K = int(rng.choice([1, 1, 2, 3, 5, 8, 10, 33, 64, 70]))
-        S = int(rng.integers(1, 61))
-        B = int(rng.integers(1, 49))
-        knobs = dict(discount=float(rng.choice([0.997, 0.9, 1.0])), rho=float(rng.choice([0.75, 0.5, 0.0])),
-                     lam=float(rng.choice([0.8, 1.0, 0.5])), delta_lb=float(rng.choice([0.01, 0.1])),
-                     pb_c_init=float(rng.choice([1.25, 2.5])), pb_c_base=float(rng.choice([19652.0, 500.0])))
-        lz = float(rng.choice([0.0, 0.3])) if A >= 2 else 0.0
-        ties = bool(rng.random() < 0.15)
-        eps = float(rng.choice([0.0, 0.25]))
-        out.append((B, A, K, S, knobs, lz, ties, eps, int(rng.integers(1 << 30))))
-    return out
-
-
 @pytest.mark.parametrize("chunk", range(4))
 def test_fuzz_small_configs_vs_port(gpu_lib, port_lib, chunk):
     """Forty seeded random configurations (A from 1 to 64, K from 1 to 70 -- chains, trees, the
@@ -742,10 +723,11 @@ def test_fuzz_small_configs_vs_port(gpu_lib, port_lib, chunk):
 
     from mazero_amd.synthetic import make_search_inputs, run_search
 
+    from fuzz_configs import fuzz_configs
     from mazero_amd._capi import MZError
 
     ran = 0
-    for i, (B, A, K, S, knobs, lz, ties, eps, s) in enumerate(_fuzz_configs(1234 + chunk, 10)):
+    for i, (B, A, K, S, knobs, lz, ties, eps, s) in enumerate(fuzz_configs(1234 + chunk, 10)):
         rng = np.random.default_rng(s)
         inp = replace(make_search_inputs(rng, B, A, S, legal_zero_frac=lz, ties=ties), noise_eps=eps)
         where = f"B={B} A={A} K={K} S={S} knobs={knobs} lz={lz} ties={ties} eps={eps}: "

@@ -96,6 +96,25 @@ def test_port_matches_reference_fresh(ref_lib, port_lib, K, A, ties, lz):
     assert_same(outs[1], outs[0], "port vs ref ")
 
 
+@pytest.mark.parametrize("chunk", range(4))
+def test_port_matches_reference_fuzz(ref_lib, port_lib, chunk):
+    """The GPU fuzz configurations (tests/fuzz_configs.py: A 1-64, K 1-70, S 1-60, B 1-48, every
+    search knob, masks, ties, noise), the CPU port against the reference ctree, bit for bit: the
+    GPU's comparison partner is pinned on the same cases."""
+    from dataclasses import replace
+
+    from fuzz_configs import fuzz_configs
+
+    for B, A, K, S, knobs, lz, ties, eps, s in fuzz_configs(1234 + chunk, 10):
+        rng = np.random.default_rng(s)
+        inp = replace(make_search_inputs(rng, B, A, S, legal_zero_frac=lz, ties=ties), noise_eps=eps)
+        outs = []
+        for lib in (ref_lib, port_lib):
+            tb = Tree_batch(inp.B, 1, A, K, inp.S, knobs["delta_lb"], inp.seed, knobs["rho"], knobs["lam"], lib=lib)
+            outs.append(run_search(tb, inp, K, knobs))
+        assert_same(outs[1], outs[0], f"port vs ref B={B} A={A} K={K} S={S} knobs={knobs}: ")
+
+
 def test_ptree_joint_action_matches_reference(ref_lib):
     """agent_num = 2 joint-action trees (upstream MAZero semantics)."""
     rng = np.random.default_rng(7)
