@@ -205,7 +205,9 @@ class _SearchLoop:
         # float16 once per search instead of once per simulation (the reference enters autocast per
         # simulation, mcts_sampled.py:150, so it casts every weight S times; the casts are identical).
         # The context opens and closes inside a capture, so the cached casts live in the graph's pool.
-        with torch.autocast("cuda", cache_enabled=True):
+        # Inside a caller's own autocast context the cache would outlive this loop (it is cleared
+        # when the outermost context exits), so there the casts stay per simulation.
+        with torch.autocast("cuda", cache_enabled=not torch.is_autocast_enabled("cuda")):
             self._simulations(model, lib, h, leaf, act, B, A, N, cur, K, S, c2, c1, disc, tau)
 
     def _simulations(self, model, lib, h, leaf, act, B, A, N, cur, K, S, c2, c1, disc, tau):

@@ -475,6 +475,32 @@ def test_driver_graph_replay_matches_oracle(K, port_lib):
 
 
 @pytest.mark.gpu
+def test_driver_inside_caller_autocast(port_lib):
+    """batch_search called inside the caller's own autocast context (the search loop then keeps the
+    casts per simulation: a cast cache would outlive the loop and its capture): eager, captured and
+    replayed searches equal the oracle driver's."""
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, B, S, cur = 3, 9, 32, 12, 0
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=1)
+    net = make_net(N, A, seed=21, device=dev)
+    rs_o, rs_d = np.random.RandomState(9), np.random.RandomState(9)
+    oracle = OracleSampledMCTS(cfg, rs_o, port_lib)
+    drv = SampledMCTS(cfg, rs_d, use_graph=True)
+    for step in range(4):
+        out, legal = make_root_batch(net, B, 64, seed=300 + step, device=dev, legal_zero_frac=0.2)
+        exp = oracle.batch_search(net, out, cur, None, N, legal, device=dev, add_noise=True)
+        with torch.autocast("cuda"):
+            got = drv.batch_search(net, out, cur, None, N, legal, device=dev, add_noise=True)
+        _compare_outputs(got, exp)
+
+
+@pytest.mark.gpu
 def test_graph_replay_after_eager_launches(port_lib):
     """A captured search graph replayed after thousands of ordinary launches (eager searches of the
     same configuration, then the oracle's eager network calls) still matches the oracle, under the
