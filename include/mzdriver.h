@@ -11,9 +11,12 @@
  * the numpy expressions on x86-64 numpy 2.x: the exponential restates numpy's float32 SIMD exp
  * (Cody-Waite reduction, rational minimax P5/Q2 with FMAs, 2^k scaling); sums restate numpy's
  * pairwise summation (8 interleaved accumulators below 128 elements); float16 inputs follow
- * numpy's half loops (every operation evaluated in float32 and rounded to half).  The one
- * exception is sampled_tau != 1 (the reference always passes 1.0, core/config.py:403-404), where
- * the power uses the device powf.
+ * numpy's half loops (every operation evaluated in float32 and rounded to half).  With
+ * sampled_tau != 1 (the reference always passes 1.0, core/config.py:403-404) the power is the
+ * correctly rounded pow of x and 1 / sampled_tau cast to the array's dtype (NEP 50).  That is
+ * numpy's result for float16 arrays (libm's powf rounded to half) and for the exponents 2 and 0.5
+ * (np.square, np.sqrt); numpy's float32 power on AVX-512 hosts is SVML's, one ulp off the
+ * correctly rounded result for about 1 in 5 inputs, and is not reproduced.
  *
  * Exported only by the product library (mazero_amd/_build/libmzmcts.so); device memory only.
  */
@@ -64,9 +67,9 @@ int mz_readback_ready(mz_batch *b, float discount);
 /* Policy glue of one simulation (mcts_sampled.py:156-161 and 169-170).
  * logits: the network's policy logits [B, num_agents, A] (row stride `row_stride` elements,
  * the current agent's A logits start at element `col_offset` of a row), dtype `dtype`.
- * probs_out, beta_out: float32 [B, A] (= [B, 1, A]). */
+ * probs_out, beta_out: float32 [B, A] (= [B, 1, A]).  sampled_tau: the Python float. */
 int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
-                   float sampled_tau, float *probs_out, float *beta_out);
+                   double sampled_tau, float *probs_out, float *beta_out);
 
 /* numpy's np.exp of every float16 bit pattern, table[bits] = bits of np.exp(half(bits)), for the
  * float16 paths of mz_policy_glue and mz_root_glue on the current device.  np.exp of a float16 array
@@ -88,10 +91,10 @@ int mz_set_half_exp_table(const uint16_t *table);
  * `col_offset`), dtype `dtype`.  legal: the agent's legal mask as int32 [B, legal_stride] (the
  * caller converts an integer/bool array whose values fit) or NULL.  noises: the Dirichlet draws
  * already converted to float32 [B, A] (np_random stays on the host).  Outputs float32 [B, A].
- * sampled_tau != 1 uses the device powf (not pinned to glibc's). */
+ * sampled_tau (the Python float) != 1: beta is a float32 array, see the power above. */
 int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
                  const int32_t *legal, int64_t legal_stride, const float *noises, double noise_eps,
-                 float sampled_tau, float *probs_out, float *beta_out, float *noises_out);
+                 double sampled_tau, float *probs_out, float *beta_out, float *noises_out);
 
 /* Estimated joint action of one simulation (mcts_sampled.py:116-147):
  *   joint[i, k] = factor[i, k]                      for k <  current_agent  (factor int32 [B, factor_cols])

@@ -108,8 +108,8 @@ MZ_DT_F32, MZ_DT_F16 = 0, 1
 DRIVER_SIGNATURES = {
     "mz_reseed": (_i, [_p, C.c_uint32]),
     "mz_state_changed": (_i, [_p]),
-    "mz_policy_glue": (_i, [_p, _p, _i, _i64, _i64, _f, _p, _p]),
-    "mz_root_glue": (_i, [_p, _p, _i, _i64, _i64, _p, _i64, _p, C.c_double, _f, _p, _p, _p]),
+    "mz_policy_glue": (_i, [_p, _p, _i, _i64, _i64, C.c_double, _p, _p]),
+    "mz_root_glue": (_i, [_p, _p, _i, _i64, _i64, _p, _i64, _p, C.c_double, C.c_double, _p, _p, _p]),
     "mz_joint_action": (_i, [_p, _p, _i, _i, _i, _p, _i, _p, _p]),
     "mz_graph_census": (_i, [_p, C.POINTER(_i), C.POINTER(_i)]),
     "mz_fused_kernel": (_i, [_p, C.c_char_p, _i]),

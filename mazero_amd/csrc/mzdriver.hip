@@ -123,6 +123,27 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// numpy's `x ** e` for an array x >= 0 of the logits' dtype and the exponent e = 1 / sampled_tau,
+// which NEP 50 casts to that dtype (the caller passes it so rounded).  numpy's exponents 2 and 0.5
+// are np.square / np.sqrt, its float16 loop is libm's powf rounded to half, and libm's powf is
+// correctly rounded in all but ~0.07 % of inputs: the float64 pow rounded to float is the correctly
+// rounded result (up to results within a float64 ulp of a float midpoint), so all of these agree
+// with it.  numpy's float32 loop on AVX-512 hosts is SVML's powf, which is not correctly rounded
+// (about 1 in 5 results is one ulp off); that case is not reproducible here.
+// use_pow: 0 no power (exponent 1.0: numpy returns the array), kPowSquare / kPowSqrt (numpy's
+// fast_scalar_power for the Python exponents 2.0 and 0.5), kPowGeneral
+constexpr int kPowGeneral = 1, kPowSquare = 2, kPowSqrt = 3;
+template <bool F16>
+__device__ __forceinline__ float np_pow_as(float x, float e, int mode) {
+    if (mode == kPowSquare) return round_as<F16>(x * x);
+    if (mode == kPowSqrt) return round_as<F16>(sqrtf(x));  // (IEEE: -fhip-fp32-correctly-rounded-divide-sqrt)
+    return round_as<F16>((float)pow((double)x, (double)e));
+}
+
+int pow_mode(double inv) {
+    return inv == 1.0 ? 0 : inv == 2.0 ? kPowSquare : inv == 0.5 ? kPowSqrt : kPowGeneral;
+}
+
 // mcts_sampled.py:158-161 (+ .astype(np.float32), :169-170) for root blockIdx.x.
 template <bool F16>
 __global__ __launch_bounds__(kWave) void k_policy_glue(const void *logits, long long row_stride, long long col_off,
@@ -142,7 +163,7 @@ __global__ __launch_bounds__(kWave) void k_policy_glue(const void *logits, long 
     const float s = round_as<F16>(np_row_sum(e, l, A, lds, acc));
     const float p = round_as<F16>(e / s);
     // `** (1 / sampled_tau)`: numpy returns the array itself for an exponent of 1.0
-    const float q = use_pow ? round_as<F16>(powf(p, tau_inv)) : p;
+    const float q = use_pow ? np_pow_as<F16>(p, tau_inv, use_pow) : p;
     const float s2 = round_as<F16>(np_row_sum(q, l, A, lds, acc));
     const float b = round_as<F16>(q / s2);
     if (on) {
@@ -240,7 +261,7 @@ __global__ __launch_bounds__(kWave) void k_root_glue(const void *logits, long lo
     const float c1 = store_d<F16>(one_minus_eps), c2 = (float)eps;
     const float a1 = round_as<F16>(p * c1);
     float b = a1 + n * c2;
-    if (use_pow) b = powf(b, tau_inv);
+    if (use_pow) b = np_pow_as<false>(b, tau_inv, use_pow);  // a float32 array
     if (legal) b = (float)((double)b * lg);
     const float sb = np_row_sum(b, l, A, lds, acc);
     b = b / sb;
@@ -312,7 +333,7 @@ int mz_set_half_exp_table(const uint16_t *table) {
 }
 
 int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
-                   float sampled_tau, float *probs_out, float *beta_out) {
+                   double sampled_tau, float *probs_out, float *beta_out) {
     int B = 0, A = 0;
     hipStream_t stream = nullptr;
     int rc = mz_internal_launch_info(b, &B, &A, &stream);
@@ -321,9 +342,10 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
     if (dtype != MZ_DT_F32 && dtype != MZ_DT_F16) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: bad dtype");
     if (row_stride < A || col_offset < 0 || col_offset + A > row_stride)
         return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: logits row does not hold the agent's actions");
-    if (!(sampled_tau > 0.f)) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: sampled_tau must be > 0");
-    const float tau_inv = (float)(1.0 / (double)sampled_tau);
-    const int use_pow = (1.0 / (double)sampled_tau) != 1.0;
+    if (!(sampled_tau > 0.0)) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: sampled_tau must be > 0");
+    const double inv = 1.0 / sampled_tau;  // Python's `1 / sampled_tau`, cast to the array's dtype
+    const float tau_inv = (dtype == MZ_DT_F16) ? (float)(_Float16)inv : (float)inv;
+    const int use_pow = pow_mode(inv);
     if (dtype == MZ_DT_F16)
         hipLaunchKernelGGL(k_policy_glue<true>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,
                            (long long)col_offset, A, use_pow, tau_inv, probs_out, beta_out, half_exp_table());
@@ -338,7 +360,7 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
 
 int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride, int64_t col_offset,
                  const int32_t *legal, int64_t legal_stride, const float *noises, double noise_eps,
-                 float sampled_tau, float *probs_out, float *beta_out, float *noises_out) {
+                 double sampled_tau, float *probs_out, float *beta_out, float *noises_out) {
     int B = 0, A = 0;
     hipStream_t stream = nullptr;
     int rc = mz_internal_launch_info(b, &B, &A, &stream);
@@ -349,9 +371,10 @@ int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride,
     if (row_stride < A || col_offset < 0 || col_offset + A > row_stride)
         return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: logits row does not hold the agent's actions");
     if (legal && legal_stride < A) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: legal rows hold fewer than A");
-    if (!(sampled_tau > 0.f)) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: sampled_tau must be > 0");
-    const float tau_inv = (float)(1.0 / (double)sampled_tau);
-    const int use_pow = (1.0 / (double)sampled_tau) != 1.0;
+    if (!(sampled_tau > 0.0)) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: sampled_tau must be > 0");
+    const double inv = 1.0 / sampled_tau;  // beta is a float32 array here (:93)
+    const float tau_inv = (float)inv;
+    const int use_pow = pow_mode(inv);
     const double ome = 1.0 - noise_eps;  // (Python float arithmetic)
     if (dtype == MZ_DT_F16)
         hipLaunchKernelGGL(k_root_glue<true>, dim3(B), dim3(kWave), 0, stream, logits, (long long)row_stride,

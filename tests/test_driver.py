@@ -12,6 +12,7 @@ oracle driver running the same network on the same GPU.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import re
 
@@ -116,11 +117,25 @@ def test_numpy_float16_sum_restatement():
             assert np.float16(np_row_sum_emulated(X[i].astype(np.float32))) == S[i]
 
 
-def _numpy_policy_glue(logits, tau=1.0):
-    """mcts_sampled.py:158-161 + astype(np.float32) (:169-170), in the logits' dtype."""
+TAUS = (0.5, 2.0, 1.5, 0.3, 3.0, 0.7, 0.25, 1.1)
+
+
+def _cr_pow(x: np.ndarray, tau: float) -> np.ndarray:
+    """x ** (1 / tau) as the glue kernels evaluate it (mzdriver.hip np_pow_as): the exponent cast
+    to x's dtype (NEP 50), the float64 pow (libm, correctly rounded) rounded to float, then to x's
+    dtype."""
+    e = float(x.dtype.type(1 / tau))
+    flat = x.astype(np.float32).ravel()
+    r = np.array([math.pow(float(v), e) for v in flat], dtype=np.float32).reshape(x.shape)
+    return r.astype(x.dtype)
+
+
+def _numpy_policy_glue(logits, tau=1.0, cr_pow=False):
+    """mcts_sampled.py:158-161 + astype(np.float32) (:169-170), in the logits' dtype.  cr_pow: the
+    power correctly rounded (_cr_pow) instead of numpy's own."""
     p = np.exp(logits - np.max(logits, axis=-1, keepdims=True))
     p = p / np.sum(p, axis=-1, keepdims=True)
-    b = p ** (1 / tau)
+    b = _cr_pow(p, tau) if cr_pow and tau != 1.0 else p ** (1 / tau)
     b = b / np.sum(b, axis=-1, keepdims=True)
     return p.astype(np.float32), b.astype(np.float32)
 
@@ -172,6 +187,19 @@ def test_half_exp_table_is_numpy():
         np.testing.assert_array_equal(t[fin], np.exp(x[fin]).view(np.uint16))
 
 
+@pytest.mark.parametrize("tau", TAUS)
+def test_numpy_half_power_is_correctly_rounded(tau):
+    """numpy's float16 `p ** (1 / tau)` over every half p in [0, 1] (the softmax's range) is the
+    correctly rounded power with the exponent cast to half, which the glue kernels evaluate; and for
+    float32 arrays the exponents 2 and 0.5 (np.square / np.sqrt) are too.  numpy's other float32
+    powers are host-dependent (SVML on AVX-512 hosts, not correctly rounded)."""
+    h = np.arange(0x3C01, dtype=np.uint16).view(np.float16)
+    np.testing.assert_array_equal((h ** (1 / tau)).view(np.uint16), _cr_pow(h, tau).view(np.uint16))
+    if 1 / tau in (2.0, 0.5):
+        x = np.random.default_rng(3).random(100_000).astype(np.float32)
+        np.testing.assert_array_equal((x ** (1 / tau)).view(np.uint32), _cr_pow(x, tau).view(np.uint32))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["float32", "float16"])
 @pytest.mark.parametrize("A", [3, 9, 15, 36, 64])
@@ -201,6 +229,90 @@ def test_policy_glue_matches_numpy(dtype, A):
     gp, gb = probs.cpu().numpy(), beta.cpu().numpy()
     np.testing.assert_array_equal(gp.view(np.uint32), ep.reshape(B, A).view(np.uint32))
     np.testing.assert_array_equal(gb.view(np.uint32), eb.reshape(B, A).view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+@pytest.mark.parametrize("tau", TAUS)
+def test_policy_glue_sampled_tau(dtype, tau):
+    """sampled_tau != 1 (mcts_sampled.py:160): bit-exact against numpy for float16 logits and for
+    the float32 exponents 2 and 0.5; other float32 exponents bit-exact against the correctly
+    rounded power and within 1e-6 of this host's numpy (SVML on AVX-512 hosts)."""
+    import torch
+
+    from mazero_amd._capi import MZ_DT_F16, MZ_DT_F32, check
+
+    B, N, cur, A = 2048, 2, 1, 64
+    rng = np.random.default_rng(int(tau * 100))
+    logits = (rng.standard_normal((B, N, A)) * rng.choice([0.1, 1, 4, 12], size=(B, 1, 1))).astype(dtype)
+    logits[:5, cur, 1] = 60.0  # one dominant logit (others underflow to 0)
+    tb = _handle(B, A)
+    dev = torch.device("cuda", 0)
+    x = torch.from_numpy(logits).to(dev)
+    probs, beta = torch.empty(B, A, device=dev), torch.empty(B, A, device=dev)
+    tb._sync_stream()
+    rc = tb._lib.mz_policy_glue(tb._h, C.c_void_p(x.data_ptr()), MZ_DT_F16 if dtype == "float16" else MZ_DT_F32,
+                                N * A, cur * A, tau, C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr()))
+    check(tb._lib, rc, "policy_glue")
+    gp, gb = probs.cpu().numpy(), beta.cpu().numpy()
+    row = logits[:, cur, :].reshape(B, 1, A)
+    with np.errstate(all="ignore"):
+        ep, eb = _numpy_policy_glue(row, tau)
+        cp, cb = _numpy_policy_glue(row, tau, cr_pow=True)
+    np.testing.assert_array_equal(gp.view(np.uint32), ep.reshape(B, A).view(np.uint32))
+    np.testing.assert_array_equal(gb.view(np.uint32), cb.reshape(B, A).view(np.uint32))
+    if dtype == "float16" or 1 / tau in (2.0, 0.5):
+        np.testing.assert_array_equal(gb.view(np.uint32), eb.reshape(B, A).view(np.uint32))
+    else:
+        np.testing.assert_allclose(gb, eb.reshape(B, A), rtol=1e-6, atol=1e-30)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tau", (0.5, 2.0, 1.5))
+def test_root_glue_sampled_tau(tau):
+    """mz_root_glue with sampled_tau != 1 (mcts_sampled.py:94) against the host root preprocessing:
+    bit-exact for the exponents 2 and 0.5 (np.square / np.sqrt of the float32 beta), within 1e-6
+    otherwise (numpy's float32 power is SVML's on AVX-512 hosts)."""
+    import torch
+
+    from mazero_amd._capi import check
+    from mazero_amd.mcts_sampled import SampledMCTS
+    from mazero_amd.nets import NetworkOutput, SearchConfig
+
+    B, N, cur, A = 300, 3, 1, 15
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(17)
+    tb = _handle(B, A)
+    cfg = SearchConfig(action_space_size=A)
+    for dtype in ("float32", "float16"):
+        for legal_kind in ("none", "int64"):
+            logits = (rng.standard_normal((B, N, A)) * 3).astype(dtype)
+            legal = None
+            if legal_kind == "int64":
+                legal = (rng.random((B, N, A)) >= 0.3).astype(np.int64)
+                legal[..., 0] = 1
+            out = NetworkOutput(torch.zeros(B, 4, device=dev), rng.standard_normal((B, 1)).astype(np.float32),
+                                rng.standard_normal((B, 1)).astype(np.float32), logits)
+            m_host, m_dev = SampledMCTS(cfg, np.random.RandomState(9)), SampledMCTS(cfg, np.random.RandomState(9))
+            (rr, rv, rp, rb, eps, rn), _ = m_host.root_inputs(out, cur, legal, True, tau)
+            arrays, mode, eps_d, _ = m_dev.root_raw(out, cur, legal, True)
+            t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in arrays.items()}
+            probs, beta, nz = (torch.empty(B, A, device=dev) for _ in range(3))
+            tb._sync_stream()
+            lg = t.get("legal")
+            check(tb._lib, tb._lib.mz_root_glue(tb._h, C.c_void_p(t["logits"].data_ptr()), mode[0], A, 0,
+                                                None if lg is None else C.c_void_p(lg.data_ptr()), A,
+                                                C.c_void_p(t["noise"].data_ptr()), float(eps_d), tau,
+                                                C.c_void_p(probs.data_ptr()), C.c_void_p(beta.data_ptr()),
+                                                C.c_void_p(nz.data_ptr())), "root_glue")
+            where = f"{dtype} legal={legal_kind} tau={tau}"
+            np.testing.assert_array_equal(probs.cpu().numpy().view(np.uint32), rp.reshape(B, A).view(np.uint32),
+                                          err_msg=where)
+            gb = beta.cpu().numpy()
+            if 1 / tau in (2.0, 0.5):
+                np.testing.assert_array_equal(gb.view(np.uint32), rb.reshape(B, A).view(np.uint32), err_msg=where)
+            else:
+                np.testing.assert_allclose(gb, rb.reshape(B, A), rtol=1e-6, atol=1e-30, err_msg=where)
 
 
 def _half_exp_exceptions() -> np.ndarray:
