@@ -713,7 +713,8 @@ def test_get_roots_device_checks_outputs(gpu_lib):
     assert np.array_equal(v.cpu().numpy().view(np.int32), tb.get_roots_values().view(np.int32))
 
 
-@pytest.mark.parametrize("chunk", range(4))
+# MZ_FUZZ_CHUNKS=N widens the fuzz to N chunks of ten configurations (a one-off deeper run)
+@pytest.mark.parametrize("chunk", range(int(os.environ.get("MZ_FUZZ_CHUNKS", "4"))))
 def test_fuzz_small_configs_vs_port(gpu_lib, port_lib, chunk):
     """Forty seeded random configurations (A from 1 to 64, K from 1 to 70 -- chains, trees, the
     general kernel --, S from 1 to 60, B from 1 to 48, every search knob varied, masks, ties, noise
