@@ -96,7 +96,7 @@ def test_port_matches_reference_fresh(ref_lib, port_lib, K, A, ties, lz):
     assert_same(outs[1], outs[0], "port vs ref ")
 
 
-@pytest.mark.parametrize("chunk", range(4))
+@pytest.mark.parametrize("chunk", range(int(os.environ.get("MZ_FUZZ_CHUNKS", "4"))))  # (as the GPU fuzz)
 def test_port_matches_reference_fuzz(ref_lib, port_lib, chunk):
     """The GPU fuzz configurations (tests/fuzz_configs.py: A 1-64, K 1-70, S 1-60, B 1-48, every
     search knob, masks, ties, noise), the CPU port against the reference ctree, bit for bit: the
