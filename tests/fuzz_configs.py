@@ -23,3 +23,21 @@ def fuzz_configs(seed: int, n: int):
         eps = float(rng.choice([0.0, 0.25]))
         out.append((B, A, K, S, knobs, lz, ties, eps, int(rng.integers(1 << 30))))
     return out
+
+
+def fuzz_configs_large(seed: int, n: int):
+    """Seeded random configurations at SMAC-like sizes (S 60-300, B 64-512): the larger layout
+    classes of the chain and tree kernels and the general kernel."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        A = int(rng.choice([5, 9, 11, 14, 17, 36, 64]))
+        K = int(rng.choice([1, 1, 2, 3, 5, 8, 10, 16]))
+        S = int(rng.integers(60, 301))
+        B = int(rng.integers(64, 513))
+        knobs = dict(discount=float(rng.choice([0.997, 0.99])), rho=float(rng.choice([0.75, 0.5])),
+                     lam=float(rng.choice([0.8, 1.0])), delta_lb=0.01, pb_c_init=1.25, pb_c_base=19652.0)
+        lz = float(rng.choice([0.0, 0.3]))
+        eps = float(rng.choice([0.0, 0.25]))
+        out.append((B, A, K, S, knobs, lz, False, eps, int(rng.integers(1 << 30))))
+    return out

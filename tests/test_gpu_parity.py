@@ -747,3 +747,30 @@ def test_fuzz_small_configs_vs_port(gpu_lib, port_lib, chunk):
             host = {k: v for k, v in host.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
             assert_same(host, exp, "gpu host path " + where)
     assert ran >= 8
+
+
+@pytest.mark.parametrize("chunk", range(int(os.environ.get("MZ_FUZZ_CHUNKS", "2"))))
+def test_fuzz_large_configs_vs_port(gpu_lib, port_lib, chunk):
+    """Four seeded random configurations at SMAC-like sizes (A 5-64, K 1-16, S 60-300, B 64-512):
+    the fused device loop against the CPU port, every selection and readback; pools over the
+    per-tree LDS limit are refused at construction and skipped."""
+    from dataclasses import replace
+
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    from fuzz_configs import fuzz_configs_large
+    from mazero_amd._capi import MZError
+
+    for B, A, K, S, knobs, lz, ties, eps, s in fuzz_configs_large(777 + chunk, 4):
+        rng = np.random.default_rng(s)
+        inp = replace(make_search_inputs(rng, B, A, S, legal_zero_frac=lz, ties=ties), noise_eps=eps)
+        where = f"B={B} A={A} K={K} S={S} knobs={knobs} lz={lz} eps={eps}: "
+        try:
+            tb = make_tb(gpu_lib, inp, K, knobs)
+        except MZError as e:
+            assert "too large" in str(e) and 1 + min(K, A) * (S + 1) > 1500, where + str(e)
+            continue
+        exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
+        exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+        out, _ = run_fused(tb, to_device(inp), K, knobs)
+        assert_same(out, exp, "gpu fused " + where)
