@@ -196,7 +196,7 @@ class Tree_batch:
         """Like batch_selection but returns device int32 tensors (idx_x [B], idy [B], actions [B,N])."""
         B, N = self.root_num, self.agent_num
         if out is None:
-            dev = torch.device("cuda", torch.cuda.current_device())
+            dev = torch.device("cuda", self.device_index)  # (the arena's device)
             out = (
                 torch.empty(B, dtype=torch.int32, device=dev),
                 torch.empty(B, dtype=torch.int32, device=dev),
@@ -272,7 +272,7 @@ class Tree_batch:
 
     # -- device readbacks (no host synchronisation) -------------------------------------------
     def get_roots_values_device(self, out=None):
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cuda", self.device_index)  # (the arena's device)
         out = torch.empty(self.root_num, dtype=torch.float32, device=dev) if out is None else out
         self._sync_stream()
         check(self._lib, self._lib.mz_get_roots_values(self._h, C.c_void_p(out.data_ptr()), MZ_MEM_DEVICE),
@@ -281,7 +281,7 @@ class Tree_batch:
 
     def get_roots_marginal_device(self, visit_out=None, prior_out=None):
         """(marginal visit counts int32 [B, N, A], marginal priors f32 [B, N, A]) on the device."""
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cuda", self.device_index)  # (the arena's device)
         shape = (self.root_num, self.agent_num, self.action_space_size)
         visit_out = torch.empty(shape, dtype=torch.int32, device=dev) if visit_out is None else visit_out
         prior_out = torch.empty(shape, dtype=torch.float32, device=dev) if prior_out is None else prior_out
@@ -349,7 +349,7 @@ class Tree_batch:
         """Device form of get_roots_sampled_padded: (tensor [B, maxdeg(*N)], degrees int32 [B])."""
         B, N = self.root_num, self.agent_num
         W = self.max_children()
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cuda", self.device_index)  # (the arena's device)
         width = W * N if name == "actions" else W
         out = torch.empty(B, width, dtype=torch.int32 if name in INT_FIELDS else torch.float32, device=dev)
         self._sync_stream()
