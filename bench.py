@@ -450,7 +450,7 @@ def trace_mark(dev, k):
 
 def timed(leg, steps, world, dist, sync, dev):
     """EXACTLY `steps` env steps between barrier + device synchronisation on both sides; the max
-    over ranks of the wall time."""
+    over ranks of the wall time, and this rank's own."""
     trace_mark(dev, 1)
     if world > 1:
         dist.barrier()
@@ -459,6 +459,7 @@ def timed(leg, steps, world, dist, sync, dev):
     leg.run(steps)
     sync()
     elapsed = time.perf_counter() - t0
+    own = elapsed
     trace_mark(dev, 2)
     if world > 1:
         import torch
@@ -468,7 +469,23 @@ def timed(leg, steps, world, dist, sync, dev):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     leg.check()
-    return elapsed
+    return elapsed, own
+
+
+def rank_record(rank, local, dev, legs, steps):
+    """What one rank ran on, for the N > 1 line: its device (index, name, PCI bus id) and its own
+    ms per env step in each leg (the line's value uses the max over ranks)."""
+    rec = dict(rank=rank, local_rank=local, device=str(dev))
+    if dev.type == "cuda":
+        import torch
+
+        p = torch.cuda.get_device_properties(dev)
+        rec["device_name"] = p.name
+        bus = getattr(p, "pci_bus_id", None)
+        if bus is not None:
+            rec["pci_bus_id"] = int(bus)
+    rec["ms_per_step"] = {k: round(v["own"] / steps * 1e3, 4) for k, v in legs.items()}
+    return rec
 
 
 def main():
@@ -540,9 +557,17 @@ def main():
         leg = make_leg(inputs, off)
         leg.prepare()
         st0 = leg.stats() if hip and rank == 0 and not args.dropin else None
-        elapsed = timed(leg, args.steps, world, dist, sync, dev)
+        elapsed, own = timed(leg, args.steps, world, dist, sync, dev)
         st1 = leg.stats() if hip and rank == 0 and not args.dropin else None
-        legs[kind] = dict(leg=leg, B=B, total=total, elapsed=elapsed, st0=st0, st1=st1)
+        legs[kind] = dict(leg=leg, B=B, total=total, elapsed=elapsed, own=own, st0=st0, st1=st1)
+    # N > 1: every rank's device and its own step time, gathered to rank 0, and the collective's
+    # view of the job (the line checks itself against the launcher's world size)
+    ranks = None
+    if world > 1:
+        recs = [None] * world
+        dist.all_gather_object(recs, rank_record(rank, local, dev, legs, args.steps))
+        ranks = dict(world_size=dist.get_world_size(), backend=str(dist.get_backend()), per_rank=recs,
+                     distinct_devices=len({(r["device"], r.get("pci_bus_id")) for r in recs}))
 
     main_kind = order[0]
     m = legs[main_kind]
@@ -607,6 +632,7 @@ def main():
                 "parallelism": f"roots sharded over {world} GPU(s), no collective on the data path",
             },
             **other,
+            **({"ranks": ranks} if ranks is not None else {}),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

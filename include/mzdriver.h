@@ -118,10 +118,19 @@ int mz_graph_census(void *graph, int *total_nodes, int *memset_nodes);
 
 /* The kernel this handle launches for a fused simulation step (mz_expand_backup_select), as a
  * NUL-terminated name written into out[len]: "k_chain3<NC>", "k_chain<NC>", "k_tree<NC>",
- * "k_step<NC>" or "k_step<0,joint>" (NC = the compile-time node class, 0 = run-time layout).
- * Chosen at mz_create from the geometry (and MZ_CHAIN_V2 / MZ_NO_CHAIN / MZ_NO_TREE); for the
- * bench's roofline label and the tests that pin which path ran. */
+ * "k_step<NC>", "k_step<0,joint>" (NC = the compile-time node class, 0 = run-time layout), or
+ * "k_hbm" / "k_hbm<joint>" for pools whose LDS image exceeds one CU's 160 KB (the tree stays in the
+ * arena).  Chosen at mz_create from the geometry (and MZ_CHAIN_V2 / MZ_NO_CHAIN / MZ_NO_TREE /
+ * MZ_HBM); for the bench's roofline label and the tests that pin which path ran. */
 int mz_fused_kernel(mz_batch *b, char *out, int len);
+
+/* Release what the library keeps for reuse across handles: device arenas of destroyed handles
+ * (at most 2 GiB / 16 blocks per process, reused by a handle of the same size, as the reference's
+ * per-search Tree_batch re-creates them, mcts_sampled.py:89) and pinned host stages (at most
+ * 256 MiB).  The per-device mt19937 seeding table (~97 MB, built at the first mz_create on a
+ * device) stays.  `released` (may be NULL) receives the bytes freed.  A handle's own arena is
+ * never touched; an arena allocation that fails releases the cache and retries by itself. */
+int mz_trim_caches(int64_t *released);
 
 #ifdef __cplusplus
 }

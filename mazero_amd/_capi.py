@@ -116,6 +116,7 @@ DRIVER_SIGNATURES = {
     "mz_set_half_exp_table": (_i, [_p]),
     "mz_expand_backup_readback": (_i, [_p, _i, _f, _i, _p, _p, _p, _p, _f, _p]),
     "mz_readback_ready": (_i, [_p, _f]),
+    "mz_trim_caches": (_i, [C.POINTER(_i64)]),
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 

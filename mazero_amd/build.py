@@ -52,7 +52,7 @@ def needs_build(lib: str = LIB) -> bool:
     if not os.path.exists(lib):
         return True
     t = os.path.getmtime(lib)
-    deps = [*SRCS, os.path.join(HERE, "csrc", "mz_internal.h"), os.path.join(HERE, "csrc", "mt_seed.inc"), os.path.join(ROOT, "include", "mzmcts.h"),
+    deps = [*SRCS, os.path.join(HERE, "csrc", "mz_internal.h"), os.path.join(HERE, "csrc", "mt_seed.inc"), os.path.join(HERE, "csrc", "mzhbm.inc"), os.path.join(ROOT, "include", "mzmcts.h"),
             os.path.join(ROOT, "include", "mzdriver.h"), os.path.join(ROOT, "include", "mzconsume.h"), __file__]
     return any(os.path.getmtime(p) > t for p in deps)
 

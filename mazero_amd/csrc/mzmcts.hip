@@ -978,10 +978,14 @@ __device__ __forceinline__ unsigned mt_temper(unsigned z) {
 constexpr int kSeedStep = 16, kSeedRow = 40;
 static_assert(kMtN % kSeedStep == 0 && kMtN / kSeedStep < kSeedRow, "seeding checkpoints");
 
+// One block builds 256 consecutive rows in LDS (thread k: row v0 + k) and writes them out as one
+// contiguous 40 KB span with 16-byte stores (a thread storing its own 160-byte row directly made
+// every store instruction touch 64 rows: ~6x the table in HBM writes, round 4's PMC).
 __global__ __launch_bounds__(256) void k_seed_table(unsigned *cp, unsigned n) {
-    const unsigned v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= n) return;
-    unsigned *row = cp + (size_t)v * kSeedRow;
+    __shared__ __attribute__((aligned(16))) unsigned rows[256 * kSeedRow];
+    const unsigned v0 = blockIdx.x * 256u;
+    const unsigned v = v0 + threadIdx.x;
+    unsigned *row = rows + threadIdx.x * kSeedRow;
     unsigned x = v;
     row[0] = x;
     for (int i = 1; i < kMtN; ++i) {
@@ -989,6 +993,11 @@ __global__ __launch_bounds__(256) void k_seed_table(unsigned *cp, unsigned n) {
         if (i % kSeedStep == 0) row[i / kSeedStep] = x;
     }
     row[kSeedRow - 1] = 0u;
+    __syncthreads();
+    const unsigned nrows = (n - v0) < 256u ? (n - v0) : 256u;
+    const int4 *src = (const int4 *)rows;
+    int4 *dst = (int4 *)(cp + (size_t)v0 * kSeedRow);  // (160-byte rows: 16-byte aligned)
+    for (unsigned i = threadIdx.x; i < nrows * (kSeedRow / 4); i += 256u) dst[i] = src[i];
 }
 
 __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm, PrepArgs a) {
@@ -3707,9 +3716,11 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         // from this launch's final records.  Wave 1 left every chain node's new {visit, prior, value,
         // reward} in sA (read after the barrier above); the structure records come from HBM but the
         // leaf's, rewritten above, and the root children's probabilities from HBM (written at prepare)
+        // (a tree that failed writes an empty readback -- no children, value 0 -- rather than leave
+        // the caller's buffers as they were; the error word reports it)
         const RbDesc *rbd = (const RbDesc *)(const void *)iop->gather_out;
-        if (rbd && !err) {
-            const int4 rbn = uni4(d.Bn()[nb]);
+        if (rbd) {
+            const int4 rbn = err ? make_int4(0, 0, 0, 0) : uni4(d.Bn()[nb]);
             const int nc = nc_of(rbn.y), fc = rbn.x;
             d.o_D = pl->d.o_D;
             const int md = md_of(leaf_b.y) < 0 ? 0 : md_of(leaf_b.y);
@@ -3722,7 +3733,8 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                 cb = (n == leaf) ? leaf_new : d.Bn()[nb + n];
                 cd = d.D()[nb + n];
             }
-            readback_emit(rbd->o, rbd->disc, rbd->Wd, t, A, 1, nc, sA[0], ca, cb, cd, nullptr);
+            readback_emit(rbd->o, rbd->disc, rbd->Wd, t, A, 1, nc, err ? make_int4(0, 0, 0, 0) : sA[0], ca, cb, cd,
+                          nullptr);
         }
     }
     stamp(ts, 6);
@@ -5256,8 +5268,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         // from the state after barrier (2) -- the staged records (sA, sB), the path nodes' new value
         // and reward (sAz; flagged in sFl, one more visit), the leaf's new structure record (sB) --
         // and the root children's probabilities from HBM (written at prepare)
+        // (a tree that failed writes an empty readback, as k_chain3)
         const RbDesc *rbd = (const RbDesc *)(const void *)gather_out;
-        if (rbd && !err) {
+        if (rbd) {
             auto upd = [&](int n) {
                 int4 a = sA[n];
                 if (sFl[n]) {
@@ -5266,7 +5279,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 }
                 return a;
             };
-            const int4 rbn = uni4(sB[0]);
+            const int4 rbn = err ? make_int4(0, 0, 0, 0) : uni4(sB[0]);
             const int nc = nc_of(rbn.y), fc = rbn.x;
             int4 ca = make_int4(0, 0, 0, 0), cb = ca;
             float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -5275,7 +5288,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 cb = sB[fc + l];
                 cd = d.D()[nb + fc + l];
             }
-            readback_emit(rbd->o, rbd->disc, rbd->Wd, t, A, 1, nc, upd(0), ca, cb, cd, nullptr);
+            readback_emit(rbd->o, rbd->disc, rbd->Wd, t, A, 1, nc, err ? make_int4(0, 0, 0, 0) : upd(0), ca, cb, cd,
+                          nullptr);
         }
     }
     if (gath_lds) {
@@ -5407,6 +5421,9 @@ __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm,
     readback_emit(o, disc, Wd, t, g.A, g.N, nc, ra, ca, cb, cd, jt);
 }
 
+// pools past the per-CU LDS image: k_hbm
+#include "mzhbm.inc"
+
 }  // namespace
 
 // ================================================================================================
@@ -5447,6 +5464,7 @@ struct mz_batch {
     int chain_nc = -1;         // k_chain node class for K = 1 trees (-1: k_step for every launch)
     int chain3_nc = 0;         // k_chain3 node class (64 .. 1024) for K = 1 trees, 0: k_chain / k_step
     int tree_nc = -1;          // k_tree node class for 2 <= K <= 64 trees (-1: k_step)
+    bool hbm = false;          // the pool's LDS image exceeds a CU's LDS: every step launch is k_hbm
     Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
     // Host-memory path (the cytree numpy surface): one pinned stage per handle, laid out
     // [inputs B*(2+3NA) | selection B*(2+N) | error word | packed readback rb_words] (4-byte words).
@@ -5573,6 +5591,28 @@ struct BlockCache {
     std::mutex mu;
     std::vector<Blk> free;
     size_t held = 0;
+    // free every cached block of `device` (-1: all); returns the bytes released
+    size_t drain(int device, bool host) {
+        std::vector<Blk> out;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            for (size_t i = 0; i < free.size();)
+                if (device < 0 || free[i].device == device) {
+                    out.push_back(free[i]);
+                    held -= free[i].bytes;
+                    free.erase(free.begin() + (long)i);
+                } else {
+                    ++i;
+                }
+        }
+        size_t n = 0;
+        for (auto &b : out) {
+            if (host) (void)hipHostFree(b.p);
+            else (void)hipFree(b.p);
+            n += b.bytes;
+        }
+        return n;
+    }
     void *take(int device, size_t bytes) {
         std::lock_guard<std::mutex> g(mu);
         for (size_t i = 0; i < free.size(); ++i)
@@ -5601,7 +5641,10 @@ BlockCache &stage_cache() {
     static BlockCache *c = new BlockCache;
     return *c;
 }
-constexpr size_t kArenaCacheBytes = (size_t)4 << 30, kArenaCacheBlocks = 16;
+// (what stays resident: at most kArenaCacheBytes of released arenas and kStageCacheBytes of pinned
+// stages per process, plus the per-device seeding table of ~97 MB; mz_trim_caches releases the
+// first two, and an arena allocation that fails releases them and tries once more)
+constexpr size_t kArenaCacheBytes = (size_t)2 << 30, kArenaCacheBlocks = 16;
 constexpr size_t kStageCacheBytes = (size_t)256 << 20, kStageCacheBlocks = 32;
 
 int ensure_device(mz_batch *b) {
@@ -5693,7 +5736,13 @@ struct ArenaPlan {
     int allocate(mz_batch *b, Dev &d) {
         if (total / 256 > 0xffffffffull) return fail(MZ_ERR_UNSUPPORTED, "device arena larger than 1 TiB");
         void *q = arena_cache().take(b->device, total);
-        if (!q) HIP_TRY(hipMalloc(&q, total));
+        if (!q && hipMalloc(&q, total) != hipSuccess) {
+            // cached arenas of other sizes may be what is missing: release them, try once more
+            (void)hipGetLastError();
+            q = nullptr;
+            (void)arena_cache().drain(b->device, false);
+            HIP_TRY(hipMalloc(&q, total));
+        }
         b->allocs.push_back(q);
         b->arena_bytes = total;
         d.base = (gchar *)q;
@@ -5796,9 +5845,31 @@ void launch_tree(mz_batch *b, const StepArgs &a) {
                        a.gather_out, a.idx_x, a.idy, a.act);
 }
 
+template <bool EB, bool SEL, bool JOINT>
+void launch_hbm_t(mz_batch *b, const StepArgs &a) {
+    hipLaunchKernelGGL((k_hbm<EB, SEL, JOINT>), dim3(b->B), dim3(kHbmWaves * kWave), hbm_lds_bytes(b->N, b->NA),
+                       b->stream, b->prm, a);
+}
+template <bool JOINT>
+void launch_hbm(mz_batch *b, bool eb, bool sel, const StepArgs &a) {
+    if (eb && sel) launch_hbm_t<true, true, JOINT>(b, a);
+    else if (eb) launch_hbm_t<true, false, JOINT>(b, a);
+    else launch_hbm_t<false, true, JOINT>(b, a);
+}
+
 int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
     const Geo &g = b->geo;
     b->dirty = true;
+    if (b->hbm) {  // pools past the LDS image: every launch of the handle
+        if (b->N > 1) launch_hbm<true>(b, eb, sel, a);
+        else launch_hbm<false>(b, eb, sel, a);
+        HIP_TRY(hipGetLastError());
+        if (eb) {
+            b->rb_valid = b->rb_dev_valid = false;
+            ++b->expansions;
+        }
+        return MZ_OK;
+    }
     if (eb && b->chain3_nc > 0) {  // K = 1 trees: the three-wave chain kernel
         if (sel) {
             switch (b->chain3_nc) {
@@ -6269,11 +6340,12 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             default: g.lds = Layout<1024>::total; break;
         }
     }
-    if (g.lds > 160 * 1024) {
-        delete b;
-        return fail(MZ_ERR_UNSUPPORTED, "tree too large for the LDS-resident kernels (1 + min(K, A^N)*(S+1) nodes)");
-    }
-    if (K == 1 && N == 1 && !getenv_flag("MZ_NO_CHAIN")) {
+    // a pool whose LDS image does not fit one CU (or MZ_HBM=1 at mz_create, for tests): every step
+    // launch of the handle is k_hbm, which keeps the tree in the arena (the reference allocates
+    // K * (S + 2) nodes for any K and S, cnode.cpp:553-577)
+    b->hbm = g.lds > 160 * 1024 || getenv_flag("MZ_HBM");
+    if (b->hbm) b->nc = 0;
+    if (!b->hbm && K == 1 && N == 1 && !getenv_flag("MZ_NO_CHAIN")) {
         b->chain_nc = 0;
         for (int nc : {64, 128, 256, 512, 1024})
             if (b->P <= nc) {
@@ -6283,7 +6355,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         if (chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave > 160 * 1024) b->chain_nc = -1;
     }
     // (k_tree stages one path node's value entries per slot: E <= kBkCap)
-    if (N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE"))
+    if (!b->hbm && N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE"))
         b->tree_nc = b->nc;
     b->zc = !getenv_flag("MZ_HOST_COPY");
     b->fused_rb = !getenv_flag("MZ_NO_FUSED_READBACK");
@@ -6361,7 +6433,21 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             return fail(MZ_ERR_DEVICE, "device initialisation failed");
         }
     }
-    if (g.lds > 64 * 1024) {
+    if (b->hbm) {
+        const int hl = hbm_lds_bytes(N, b->NA);
+        if (hl > 48 * 1024) {
+            const auto attr = hipFuncAttributeMaxDynamicSharedMemorySize;
+            (void)hipFuncSetAttribute((const void *)k_hbm<true, true, true>, attr, hl);
+            (void)hipFuncSetAttribute((const void *)k_hbm<true, false, true>, attr, hl);
+            (void)hipFuncSetAttribute((const void *)k_hbm<false, true, true>, attr, hl);
+        }
+    }
+    if (N > 1) {  // k_prepare's dynamic LDS for the root's joint inputs (mz_prepare)
+        const int jl = ((12 * b->NA + 15) & ~15) + 8 * b->NA + 4 * kWave * N;
+        if (jl > 48 * 1024)
+            (void)hipFuncSetAttribute((const void *)k_prepare, hipFuncAttributeMaxDynamicSharedMemorySize, jl);
+    }
+    if (!b->hbm && g.lds > 64 * 1024) {
 #ifndef MZ_NO_JOINT
         if (N > 1) set_lds_limit<0, true>(g.lds);
         else
@@ -6428,19 +6514,23 @@ int mz_set_stream(mz_batch *b, void *stream) {
     if (ns == b->stream) return MZ_OK;
     int rc = ensure_device(b);
     if (rc) return rc;
-    rc = flush_pending(b);  // (on the old stream, ordered before the new one's work below)
-    mark_order(b);
-    if (rc) return rc;
     // The new stream waits for the eager work the handle enqueued last (order_ev, recorded behind it
-    // by that call): the old stream itself is never queried, so one the caller has destroyed since is
-    // harmless.  Not across a graph-capture boundary: a capture orders nothing outside it and may not
-    // wait on an event recorded outside it.
+    // by that call): the old stream itself is never touched -- not even to launch a staged host-memory
+    // expansion, which runs on the new stream after the wait -- so one the caller has destroyed
+    // since is harmless.  Not across a graph-capture boundary: a capture orders nothing outside it and
+    // may not wait on an event recorded outside it.
     hipStreamCaptureStatus cn = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(ns, &cn));
+    if (cn != hipStreamCaptureStatusNone && b->pend) {  // (eager work cannot enter a capture: as it was)
+        rc = flush_pending(b);
+        mark_order(b);
+        if (rc) return rc;
+    }
     if (b->order_live && cn == hipStreamCaptureStatusNone) HIP_TRY(hipStreamWaitEvent(ns, b->order_ev, 0));
     b->order_live = false;
     b->stream = ns;
-    return MZ_OK;
+    OrderMark om{b};
+    return flush_pending(b);
 }
 
 int mz_synchronize(mz_batch *b) {
@@ -6693,12 +6783,19 @@ int mz_state_changed(mz_batch *b) {
 int mz_fused_kernel(mz_batch *b, char *out, int len) {
     if (!b || !out || len < 1) return fail(MZ_ERR_ARG, "mz_fused_kernel: null argument");
     char name[48];
-    if (b->chain3_nc > 0) std::snprintf(name, sizeof name, "k_chain3<%d>", b->chain3_nc);
+    if (b->hbm) std::snprintf(name, sizeof name, b->N > 1 ? "k_hbm<joint>" : "k_hbm");
+    else if (b->chain3_nc > 0) std::snprintf(name, sizeof name, "k_chain3<%d>", b->chain3_nc);
     else if (b->chain_nc >= 0) std::snprintf(name, sizeof name, "k_chain<%d>", b->chain_nc);
     else if (b->tree_nc > 0) std::snprintf(name, sizeof name, "k_tree<%d>", b->tree_nc);
     else if (b->N > 1) std::snprintf(name, sizeof name, "k_step<0,joint>");
     else std::snprintf(name, sizeof name, "k_step<%d>", b->nc);
     std::snprintf(out, (size_t)len, "%s", name);
+    return MZ_OK;
+}
+
+int mz_trim_caches(int64_t *released) {
+    const size_t n = arena_cache().drain(-1, false) + stage_cache().drain(-1, true);
+    if (released) *released = (int64_t)n;
     return MZ_OK;
 }
 

@@ -29,8 +29,11 @@ Model interface (core/model.py:45-79): `prediction(h) -> (policy_logits [B,N,A],
 from __future__ import annotations
 
 import ctypes as C
+import os
+import threading
 import warnings
 import weakref
+from collections import OrderedDict
 from typing import List, NamedTuple, Tuple
 
 import numpy as np
@@ -145,6 +148,7 @@ class _SearchLoop:
         self.fac = torch.zeros(B, max(cur, 1), dtype=torch.int32, device=dev)
         self.pool = None
         self.leaf = None
+        self.pool_ref = None  # the shared _Pool the two above belong to (K > 1)
         self.graph = None  # None: not recorded yet; False: not replayable (capture found memset nodes)
         self.graph_nodes = None  # (nodes, memset nodes) of the recorded graph
         self.runs = 0
@@ -233,9 +237,12 @@ class _SearchLoop:
                 pass
             else:
                 if self.pool is None:
+                    # one pool per (thread, device, S, B, row, dtype), shared by the agent loops of a
+                    # geometry: searches on one thread run one after the other, and every search
+                    # writes slot 0 and slots 1..S before it reads them
                     pdt = torch.promote_types(self.root.dtype, nh.dtype)
-                    self.pool = torch.empty((S + 1, B, nh.shape[1]), dtype=pdt, device=self.dev)
-                    self.leaf = torch.empty((B, nh.shape[1]), dtype=pdt, device=self.dev)
+                    self.pool_ref = _shared_pool(self.dev, S, B, nh.shape[1], pdt)
+                    self.pool, self.leaf = self.pool_ref.pool, self.pool_ref.leaf
                 if s == 0:
                     self.pool[0].copy_(self.root)
                 self.pool[s + 1].copy_(nh)  # :164
@@ -284,8 +291,55 @@ class _SearchLoop:
         return True
 
 
-_LOOPS: dict = {}
+# Search-loop caches.  The reference builds a new Tree_batch and a new hidden-state pool per search
+# (mcts_sampled.py:86,89) and frees both when the search returns; here a search geometry keeps its
+# device arena (_TREES), each agent loop its captured graph (_LOOPS), and the loops of one geometry
+# share one hidden-state pool (_POOLS), so that a 27-agent self-play step holds one [S+1, B, N*H]
+# pool, not 27.  Every key carries the calling thread: two threads never share a handle (a handle is
+# single-threaded, include/mzmcts.h) or a pool.  Both caches are LRU-bounded (MZ_MAX_TREES,
+# MZ_MAX_LOOPS); release() empties them.
+_LOCK = threading.RLock()
+_LOOPS: "OrderedDict" = OrderedDict()
+_TREES: "OrderedDict" = OrderedDict()
+_POOLS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+_MAX_LOOPS = int(os.environ.get("MZ_MAX_LOOPS", "64"))  # >= the agents of one self-play step
+_MAX_TREES = int(os.environ.get("MZ_MAX_TREES", "8"))
 _HALF_EXP: set = set()  # (library, device index) pairs holding the host's float16 exp table
+
+
+class _Pool:
+    """A hidden-state pool [S+1, B, cols] and its leaf-row buffer [B, cols]; freed when the last loop
+    holding it goes."""
+
+    __slots__ = ("pool", "leaf", "__weakref__")
+
+    def __init__(self, pool, leaf):
+        self.pool, self.leaf = pool, leaf
+
+
+def _shared_pool(dev, S: int, B: int, cols: int, dtype) -> _Pool:
+    key = (threading.get_ident(), str(dev), S + 1, B, int(cols), dtype)
+    with _LOCK:
+        p = _POOLS.get(key)
+        if p is None:
+            p = _Pool(torch.empty((S + 1, B, cols), dtype=dtype, device=dev), torch.empty((B, cols), dtype=dtype, device=dev))
+            _POOLS[key] = p
+        return p
+
+
+def _evict_loops_of(tb) -> None:
+    for k in [k for k, v in _LOOPS.items() if v.tb is tb]:
+        del _LOOPS[k]
+
+
+def release() -> None:
+    """Drop every cached tree handle, search loop (its graph) and hidden-state pool, of every thread
+    (what the reference frees after each search, mcts_sampled.py:86,89).  The next search of a
+    geometry allocates and records again."""
+    with _LOCK:
+        _LOOPS.clear()
+        _TREES.clear()
+        _POOLS.clear()
 
 
 def half_exp_table() -> np.ndarray:
@@ -312,10 +366,10 @@ def _storage_signature(model) -> tuple:
     return tuple(t.data_ptr() for t in model.parameters()) + tuple(t.data_ptr() for t in model.buffers())
 
 
-# One device arena per search geometry, kept across searches and across SampledMCTS instances (the
-# self-play worker makes a new SampledMCTS every environment step, selfplay_worker.py:187); a
-# search reseeds it instead of allocating a new tree batch as the reference does (:89).
-_TREES: dict = {}
+# One device arena per search geometry and thread, kept across searches and across SampledMCTS
+# instances (the self-play worker makes a new SampledMCTS every environment step,
+# selfplay_worker.py:187); a search reseeds it instead of allocating a new tree batch as the
+# reference does (:89).
 
 
 class SampledMCTS:
@@ -437,18 +491,23 @@ class SampledMCTS:
         cfg = self.config
         # (pb_c_base, pb_c_init) select the handle's pUCT tables, which a graph replay does not
         # rewrite: a handle serves one pair only
-        key = (B, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
+        key = (threading.get_ident(), B, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
                float(cfg.tree_value_stat_delta_lb), float(cfg.mcts_rho), float(cfg.mcts_lambda),
                float(cfg.pb_c_base), float(cfg.pb_c_init), str(device), id(self._lib), self._root_offset())
-        tb = _TREES.get(key)
-        if tb is None:
-            tb = Tree_batch(B, 1, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
-                            cfg.tree_value_stat_delta_lb, int(seed), cfg.mcts_rho, cfg.mcts_lambda,
-                            root_offset=self._root_offset(), lib=self._lib)
-            _TREES[key] = tb
-        else:
-            tb.reseed(int(seed))
-        return tb
+        with _LOCK:
+            tb = _TREES.get(key)
+            if tb is None:
+                tb = Tree_batch(B, 1, cfg.action_space_size, cfg.sampled_action_times, cfg.num_simulations,
+                                cfg.tree_value_stat_delta_lb, int(seed), cfg.mcts_rho, cfg.mcts_lambda,
+                                root_offset=self._root_offset(), lib=self._lib)
+                _TREES[key] = tb
+                while len(_TREES) > max(_MAX_TREES, 1):  # least recently used first, with its loops
+                    _, old = _TREES.popitem(last=False)
+                    _evict_loops_of(old)
+            else:
+                _TREES.move_to_end(key)
+                tb.reseed(int(seed))
+            return tb
 
     def _root_offset(self) -> int:
         return 0 if self.root_shard is None else self.root_shard[0]
@@ -490,17 +549,21 @@ class SampledMCTS:
         with torch.cuda.device(dev):
             tb = self._tree(B, seed, dev)
             # the discount is a kernel argument of the recorded launches
-            key = (id(tb), id(model), N, cur, float(eps), float(sampled_tau), float(disc), tuple(hidden.shape),
-                   hidden.dtype, root_mode)
-            for k in [k for k, v in _LOOPS.items() if v.model_ref() is None]:
-                del _LOOPS[k]  # loops (graph, pool) of models that no longer exist
-            st = _LOOPS.get(key)
-            sig = _storage_signature(model)
-            # ids are reused once an object is freed; a recorded graph reads the parameters at the
-            # addresses it was recorded with (re-homed weights, weights.FlatWeights, need a new one)
-            if st is None or st.model_ref() is not model or st.storage != sig:
-                st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model, root_mode)
-                st.storage = sig
+            key = (threading.get_ident(), id(tb), id(model), N, cur, float(eps), float(sampled_tau), float(disc),
+                   tuple(hidden.shape), hidden.dtype, root_mode)
+            with _LOCK:
+                for k in [k for k, v in _LOOPS.items() if v.model_ref() is None]:
+                    del _LOOPS[k]  # loops (graph, pool) of models that no longer exist
+                st = _LOOPS.get(key)
+                sig = _storage_signature(model)
+                # ids are reused once an object is freed; a recorded graph reads the parameters at the
+                # addresses it was recorded with (re-homed weights, weights.FlatWeights, need a new one)
+                if st is None or st.model_ref() is not model or st.storage != sig or st.tb is not tb:
+                    st = _LOOPS[key] = _SearchLoop(tb, B, A, N, cur, hidden, dev, model, root_mode)
+                    st.storage = sig
+                _LOOPS.move_to_end(key)
+                while len(_LOOPS) > max(_MAX_LOOPS, 1):  # least recently used first
+                    _LOOPS.popitem(last=False)
             st.load(hidden, root_arrays, factor)
             with torch.no_grad():
                 if self.use_graph and st.runs > 0 and st.graph is None:

@@ -16,7 +16,7 @@ Runs in the build container (it needs oracle/_ref/libmzref.so, the reference ctr
                                     reference's selection idx/action of every simulation and all
                                     final readbacks
 
-Usage:  make -C oracle && python oracle/gen_golden.py [--full]
+Usage:  make -C oracle && python oracle/gen_golden.py [--full] [--only name,name]
 """
 from __future__ import annotations
 
@@ -56,6 +56,9 @@ CONFIGS = {
     "27m_k40": (4, 36, 40, 30, 0.25, 0.0, False, {}),
     "knobs_rho03": (8, 9, 5, 50, 0.25, 0.0, False, dict(rho=0.3, lam=0.9, delta_lb=0.05)),
     "knobs_rho0": (8, 9, 3, 40, 0.25, 0.0, False, dict(rho=0.0, lam=1.0, discount=0.99)),
+    # pools whose LDS image exceeds a CU's 160 KB (round 5: k_hbm; refused at construction before)
+    "big_a64_k70_s60": (3, 64, 70, 60, 0.25, 0.3, False, {}),
+    "big_27m_k16_s200": (2, 36, 16, 200, 0.25, 0.0, False, {}),
 }
 
 
@@ -157,11 +160,15 @@ def main():
             p = record_full(lib, name, seed=5000 + i)
             print("wrote", os.path.relpath(p, ROOT), os.path.getsize(p), "bytes", flush=True)
         return
+    only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
     for i, (name, cfg) in enumerate(CONFIGS.items()):
+        if only is not None and name not in only:
+            continue
         p = record(lib, name, cfg, seed=1000 + i)
         print("wrote", os.path.relpath(p, ROOT), os.path.getsize(p), "bytes")
-    kat()
-    print("wrote tests/golden/kat_libstdcxx.json")
+    if only is None:
+        kat()
+        print("wrote tests/golden/kat_libstdcxx.json")
 
 
 if __name__ == "__main__":

@@ -60,6 +60,17 @@ def test_gpus_flag_spawns_ranks(port_lib):
     wk = line["weak_scaling"]
     assert wk["roots_total"] == 16 and wk["roots_per_gpu"] == 8 and wk["value"] > 0
     assert line["value"] > 0
+    # the line verifies itself: the collective's world size, every rank's device and own step time
+    # in both legs; the headline ms_per_step is the max over ranks
+    rk = line["ranks"]
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo"
+    assert [r["rank"] for r in rk["per_rank"]] == [0, 1]
+    assert [r["local_rank"] for r in rk["per_rank"]] == [0, 1]
+    for r in rk["per_rank"]:
+        assert set(r["ms_per_step"]) == {"strong", "weak"} and min(r["ms_per_step"].values()) > 0
+        assert r["device"] == "cpu"
+    assert abs(max(r["ms_per_step"]["strong"] for r in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
+    assert abs(max(r["ms_per_step"]["weak"] for r in rk["per_rank"]) - wk["ms_per_step"]) < 1e-3
     # --weak: the weak leg is the headline, under a metric string that names its 16 roots
     r = subprocess.run(base + ["--weak"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -717,6 +717,65 @@ def test_captured_memset_node_keeps_loop_eager(port_lib):
             assert memsets == 0 and isinstance(lp.graph, torch.cuda.CUDAGraph)
 
 
+@pytest.mark.gpu
+def test_agent_loops_share_one_pool(port_lib):
+    """A 27-agent self-play step at K = 5 (27m-shaped: 27 agents x 36 actions, H = 128 per agent)
+    holds ONE hidden-state pool [S+1, B, N*H] for its 27 agent loops, not one per loop (round 4
+    held ~19 GB at 256 x 200); a second root count adds one pool of its own; release() frees both.
+    The reference frees its pool after every search (mcts_sampled.py:86,89).  Agents 0, 1 and 26
+    are checked against the oracle driver bit for bit."""
+    import gc
+
+    import torch
+
+    from driver import OracleSampledMCTS
+    from mazero_amd import mcts_sampled as ms
+    from mazero_amd.nets import SearchConfig, make_net, make_root_batch
+
+    N, A, S, K = 27, 36, 60, 5
+    dev = torch.device("cuda", 0)
+    cfg = SearchConfig(action_space_size=A, num_simulations=S, sampled_action_times=K)
+    net = make_net(N, A, seed=61, device=dev)
+    ms.release()
+    gc.collect()
+    torch.cuda.synchronize()
+
+    def pool_bytes(B):
+        return (S + 1) * B * N * net.hidden * 4
+
+    def step(B):
+        out, legal = make_root_batch(net, B, 64, seed=B, device=dev, legal_zero_frac=0.2)
+        rs_o, rs_d = np.random.RandomState(B), np.random.RandomState(B)
+        oracle, drv = OracleSampledMCTS(cfg, rs_o, port_lib), ms.SampledMCTS(cfg, rs_d)
+        acts = np.zeros((B, N), np.int32)
+        mem = []
+        for agent in range(N):
+            fac = acts[:, :agent].copy() if agent else None
+            got = drv.batch_search(net, out, agent, fac, N, legal, device=dev, add_noise=True)
+            if agent in (0, 1, N - 1):
+                exp = oracle.batch_search(net, out, agent, fac, N, legal, device=dev, add_noise=True)
+                _compare_outputs(got, exp)
+            else:  # (the oracle's np_random must advance as the driver's)
+                rs_o.set_state(rs_d.get_state())
+            acts[:, agent] = [int(a[np.argmax(v), 0]) for a, v in zip(got.sampled_actions, got.sampled_visit_count)]
+            torch.cuda.synchronize()
+            mem.append(torch.cuda.memory_allocated())
+        return mem
+
+    base = torch.cuda.memory_allocated()
+    m1 = step(256)
+    assert m1[0] - base >= pool_bytes(256)  # the first loop made the pool
+    # ... and the 26 other loops share it (their own buffers are [B, N*H] each)
+    assert m1[-1] - m1[0] < pool_bytes(256), (m1[0], m1[-1], pool_bytes(256))
+    m2 = step(128)
+    assert m2[-1] - m1[-1] < pool_bytes(128) + pool_bytes(256), (m1[-1], m2[-1])
+    assert len({id(v.pool_ref) for v in ms._LOOPS.values() if v.pool_ref is not None}) == 2
+    ms.release()
+    gc.collect()
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated() - base < pool_bytes(128), (base, torch.cuda.memory_allocated())
+
+
 # ------------------------------------------------------------------------------------------------
 # Reference-driver fixtures (oracle/gen_driver_golden.py: core/mcts/tree_search/mcts_sampled.py
 # itself, imported in the build container, over the reference ctree)

@@ -158,6 +158,42 @@ def test_baseline_sizes_vs_reference(gpu_lib, path):
     assert_same(out, expected, f"gpu {os.path.basename(path)} ")
 
 
+HBM_FULL = [p for p in FULL if os.path.basename(p) in (
+    "full_3m_k1.npz", "full_3m_k5.npz", "full_3m_k5_ties.npz", "full_3s5z_k10.npz", "full_27m_k5.npz",
+    "full_3s5z_k5_legal30.npz")]
+
+
+@pytest.mark.parametrize("path", HBM_FULL, ids=[os.path.basename(p)[5:-4] for p in HBM_FULL])
+def test_hbm_kernel_vs_reference(gpu_lib, path, monkeypatch):
+    """The HBM-resident kernel (k_hbm, forced with MZ_HBM=1 at mz_create) on BASELINE-size fixtures
+    recorded from the reference ctree: every selection and readback bit for bit, through the fused
+    loop and the fused readback."""
+    inp, K, expected = load_full(path)
+    monkeypatch.setenv("MZ_HBM", "1")
+    tb = make_tb(gpu_lib, inp, K, {})
+    monkeypatch.delenv("MZ_HBM")
+    assert tb.fused_kernel() == "k_hbm"
+    out, _ = run_fused(tb, to_device(inp), K, {}, fused_rb="packed")
+    assert_same(out, expected, f"gpu k_hbm {os.path.basename(path)} ")
+
+
+@pytest.mark.parametrize("path", TRACES, ids=IDS)
+def test_hbm_kernel_golden_traces(gpu_lib, path, monkeypatch):
+    """k_hbm (MZ_HBM=1) on every golden trace: the host path (per-call selection, its
+    per-simulation readbacks) and the fused device loop."""
+    from mazero_amd.synthetic import run_search
+
+    inp, knobs, K, expected = load_trace(path)
+    monkeypatch.setenv("MZ_HBM", "1")
+    tb, tb2 = make_tb(gpu_lib, inp, K, knobs), make_tb(gpu_lib, inp, K, knobs)
+    monkeypatch.delenv("MZ_HBM")
+    assert tb.fused_kernel() == "k_hbm"
+    assert_same(run_search(tb, inp, K, knobs), expected, "gpu k_hbm (host) ")
+    out, _ = run_fused(tb2, to_device(inp), K, knobs)
+    expected = {k: v for k, v in expected.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, expected, "gpu k_hbm (fused) ")
+
+
 BIG = [
     ("3m_k1", 256, 9, 1, 50, 0.0),
     ("3m_k5", 256, 9, 5, 50, 0.3),
@@ -188,6 +224,11 @@ BIG = [
     # 512-entry value chunks (mz_create's second layout): K = 10 at S = 200
     ("k10_s200_general", 16, 9, 10, 200, 0.3),
     ("27m_k10_s200", 8, 36, 10, 200, 0.0),
+    # pools whose LDS image exceeds one CU's 160 KB: the HBM-resident kernel (refused before round 5;
+    # the reference allocates K * (S + 2) nodes for any K and S, cnode.cpp:553-577)
+    ("hbm_a64_k70_s60", 32, 64, 70, 60, 0.3),      # 3,905 reachable nodes
+    ("hbm_27m_k16_s200", 64, 36, 16, 200, 0.0),    # 3,217
+    ("hbm_k1_s2300", 2, 9, 1, 2300, 0.0),          # a K = 1 chain of 2,302 nodes (path records past 64 levels)
 ]
 
 
@@ -195,7 +236,8 @@ BIG = [
 BIG_KERNEL = {"3m_k1": "k_chain3<64>", "27m_k1": "k_chain3<256>", "k1_chain512": "k_chain<512>",
               "k1_chain1024": "k_chain<1024>", "k1_chain_general": "k_chain<0>",
               "27m_k8_general_layout": "k_step<0>", "k2_long_value_sets": "k_step<1024>",
-              "k10_s200_general": "k_step<0>", "27m_k10_s200": "k_step<0>"}
+              "k10_s200_general": "k_step<0>", "27m_k10_s200": "k_step<0>", "hbm_a64_k70_s60": "k_hbm",
+              "hbm_27m_k16_s200": "k_hbm", "hbm_k1_s2300": "k_hbm"}
 
 
 @pytest.mark.parametrize("name,B,A,K,S,lz", BIG, ids=[b[0] for b in BIG])
@@ -254,7 +296,7 @@ FUSED_RB = [
     ("chain3", 64, 9, 1, 30, None), ("chain3_s1", 64, 9, 1, 1, None), ("tree", 64, 9, 5, 30, None),
     ("tree_s1", 64, 9, 5, 1, None), ("tree_k10", 32, 15, 10, 40, None), ("chain_v2", 64, 9, 1, 30, "MZ_CHAIN_V2"),
     ("kstep_k70", 16, 64, 70, 12, None), ("chain512", 16, 9, 1, 300, None),
-    ("unfused_env", 64, 9, 5, 30, "MZ_NO_FUSED_READBACK"),
+    ("unfused_env", 64, 9, 5, 30, "MZ_NO_FUSED_READBACK"), ("hbm", 16, 64, 70, 12, "MZ_HBM"),
 ]
 
 
@@ -453,6 +495,40 @@ def test_rebind_after_bound_stream_destroyed(gpu_lib, port_lib):
     assert_same(out, exp, "gpu rebind ")
 
 
+def test_rebind_with_staged_expansion_after_stream_destroyed(gpu_lib, port_lib):
+    """A host-memory batch_expansion_and_backup is only staged (launched by the handle's next
+    call).  Staged while the handle is bound to a raw HIP stream that is then destroyed, it must be
+    launched on the stream the handle is rebound to, never on the destroyed one: the
+    search finishes on torch's stream, bit-exact against the port."""
+    import ctypes as C
+
+    from mazero_amd.synthetic import DEFAULTS, make_search_inputs, readbacks, run_search
+
+    B, A, K, S = 32, 9, 5, 16
+    inp = make_search_inputs(np.random.default_rng(78), B, A, S)
+    exp = run_search(make_tb(port_lib, inp, K, {}), inp, K, {}, per_sim=False)
+    hip = C.CDLL("libamdhip64.so.7")
+    raw = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(raw)) == 0
+    c2, c1, g = DEFAULTS["pb_c_base"], DEFAULTS["pb_c_init"], DEFAULTS["discount"]
+    torch.cuda.synchronize()
+    tb = make_tb(gpu_lib, inp, K, {})
+    sels = []
+    with torch.cuda.stream(torch.cuda.ExternalStream(raw.value)):
+        tb.prepare(inp.root_reward, inp.root_value, inp.root_policy, inp.root_beta, K, inp.noise_eps, inp.root_noise)
+        for s in range(S // 2):
+            sels.append(tb.batch_selection(c2, c1, g)[0])
+            tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+    assert hip.hipStreamDestroy(raw) == 0  # the last expansion is still staged
+    for s in range(S // 2, S):
+        sels.append(tb.batch_selection(c2, c1, g)[0])
+        tb.batch_expansion_and_backup(s + 1, g, K, inp.reward[s], inp.value[s], inp.policy[s], inp.beta[s])
+    out = dict(sel_idx=np.asarray(sels, np.int32))
+    out.update(readbacks(tb, g))
+    exp.pop("sel_act")
+    assert_same(out, exp, "gpu rebind (staged) ")
+
+
 def test_too_many_simulations_raise(gpu_lib):
     """The reference's pools are sized for simulation_num; overrunning them is reported as a
     RuntimeError at the call that overflows (host path is synchronous like the reference)."""
@@ -527,6 +603,7 @@ JOINT = [
     ("n5_k10_keywrap", 16, 5, 11, 10, 20),  # 23333^5 overflows int64: two's-complement key order
     ("n6_a4_k16", 8, 6, 4, 16, 15),
     ("n2_a1", 4, 2, 1, 3, 10),               # single-action agents draw no engine words
+    ("n2_k64_s60_hbm", 8, 2, 9, 64, 60),     # 3,905-node pools: k_hbm<joint>
 ]
 
 
@@ -558,8 +635,12 @@ def _joint_run(lib, B, N, A, K, S, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,B,N,A,K,S", JOINT, ids=[j[0] for j in JOINT])
-def test_joint_action_trees_vs_port(gpu_lib, port_lib, name, B, N, A, K, S):
+@pytest.mark.parametrize("hbm", [False, True], ids=["lds", "hbm"])
+def test_joint_action_trees_vs_port(gpu_lib, port_lib, name, B, N, A, K, S, hbm, monkeypatch):
+    if hbm:
+        monkeypatch.setenv("MZ_HBM", "1")
     rec_g, out_g = _joint_run(gpu_lib, B, N, A, K, S, 3)
+    monkeypatch.delenv("MZ_HBM", raising=False)
     rec_c, out_c = _joint_run(port_lib, B, N, A, K, S, 3)
     for s, ((ig, ag), (ic, ac)) in enumerate(zip(rec_g, rec_c)):
         np.testing.assert_array_equal(ig, ic, err_msg=f"idx sim {s}")
@@ -725,19 +806,21 @@ def test_fuzz_small_configs_vs_port(gpu_lib, port_lib, chunk):
     from mazero_amd.synthetic import make_search_inputs, run_search
 
     from fuzz_configs import fuzz_configs
-    from mazero_amd._capi import MZError
 
-    ran = 0
     for i, (B, A, K, S, knobs, lz, ties, eps, s) in enumerate(fuzz_configs(1234 + chunk, 10)):
         rng = np.random.default_rng(s)
         inp = replace(make_search_inputs(rng, B, A, S, legal_zero_frac=lz, ties=ties), noise_eps=eps)
         where = f"B={B} A={A} K={K} S={S} knobs={knobs} lz={lz} ties={ties} eps={eps}: "
+        # every configuration is accepted (pools past the LDS image take k_hbm); every third one is
+        # also forced onto k_hbm
+        if i % 3 == 1:
+            os.environ["MZ_HBM"] = "1"
         try:
             tb = make_tb(gpu_lib, inp, K, knobs)
-        except MZError as e:  # (a pool whose LDS image exceeds 160 KB: DESIGN.md §9's size limit)
-            assert "too large" in str(e) and 1 + min(K, A) * (S + 1) > 1500, where + str(e)
-            continue
-        ran += 1
+        finally:
+            os.environ.pop("MZ_HBM", None)
+        big = 1 + min(K, A) * (S + 1) > 2300
+        assert tb.fused_kernel() == "k_hbm" or not big, where + tb.fused_kernel()
         exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
         exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
         out, _ = run_fused(tb, to_device(inp), K, knobs)
@@ -746,30 +829,24 @@ def test_fuzz_small_configs_vs_port(gpu_lib, port_lib, chunk):
             host = run_search(make_tb(gpu_lib, inp, K, knobs), inp, K, knobs)
             host = {k: v for k, v in host.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
             assert_same(host, exp, "gpu host path " + where)
-    assert ran >= 8
 
 
 @pytest.mark.parametrize("chunk", range(int(os.environ.get("MZ_FUZZ_CHUNKS", "2"))))
 def test_fuzz_large_configs_vs_port(gpu_lib, port_lib, chunk):
     """Four seeded random configurations at SMAC-like sizes (A 5-64, K 1-16, S 60-300, B 64-512):
-    the fused device loop against the CPU port, every selection and readback; pools over the
-    per-tree LDS limit are refused at construction and skipped."""
+    the fused device loop against the CPU port, every selection and readback; none is refused
+    (pools over the per-tree LDS limit take k_hbm)."""
     from dataclasses import replace
 
     from mazero_amd.synthetic import make_search_inputs, run_search
 
     from fuzz_configs import fuzz_configs_large
-    from mazero_amd._capi import MZError
 
     for B, A, K, S, knobs, lz, ties, eps, s in fuzz_configs_large(777 + chunk, 4):
         rng = np.random.default_rng(s)
         inp = replace(make_search_inputs(rng, B, A, S, legal_zero_frac=lz, ties=ties), noise_eps=eps)
         where = f"B={B} A={A} K={K} S={S} knobs={knobs} lz={lz} eps={eps}: "
-        try:
-            tb = make_tb(gpu_lib, inp, K, knobs)
-        except MZError as e:
-            assert "too large" in str(e) and 1 + min(K, A) * (S + 1) > 1500, where + str(e)
-            continue
+        tb = make_tb(gpu_lib, inp, K, knobs)
         exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
         exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
         out, _ = run_fused(tb, to_device(inp), K, knobs)

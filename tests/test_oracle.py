@@ -211,4 +211,4 @@ print("sanitized replays", n)
 """
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
-    assert "sanitized replays 19" in r.stdout
+    assert f"sanitized replays {len(golden_traces()) + 3}" in r.stdout
