@@ -488,10 +488,27 @@ def rank_record(rank, local, dev, legs, steps):
     return rec
 
 
+def segv_maps():
+    """MZ_SEGV_MAPS=<file> (profiler-crash diagnosis only): on SIGSEGV the faulting address, PC,
+    thread and /proc/self/maps go to <file> (scripts/segv_maps.c), then the profiler's own handler
+    runs; a run that completes writes the maps to <file>.exit at exit."""
+    path = os.environ.get("MZ_SEGV_MAPS")
+    if not path:
+        return
+    import atexit
+    import ctypes
+
+    so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "_segv_maps.so")
+    lib = ctypes.CDLL(so)
+    lib.mz_segv_maps_install(path.encode())
+    atexit.register(lambda: lib.mz_segv_maps_snapshot((path + ".exit").encode()))
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args))
+    segv_maps()
     import torch
     import torch.distributed as dist
 

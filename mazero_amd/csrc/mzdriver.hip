@@ -338,6 +338,8 @@ int mz_policy_glue(mz_batch *b, const void *logits, int dtype, int64_t row_strid
     hipStream_t stream = nullptr;
     int rc = mz_internal_launch_info(b, &B, &A, &stream);
     if (rc) return rc;
+    if (A > kWave)  // (one lane per action; the tree itself takes up to 255 actions)
+        return mz_internal_fail(MZ_ERR_UNSUPPORTED, "mz_policy_glue: action_space_size > 64");
     if (!logits || !probs_out || !beta_out) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: null buffer");
     if (dtype != MZ_DT_F32 && dtype != MZ_DT_F16) return mz_internal_fail(MZ_ERR_ARG, "mz_policy_glue: bad dtype");
     if (row_stride < A || col_offset < 0 || col_offset + A > row_stride)
@@ -365,6 +367,8 @@ int mz_root_glue(mz_batch *b, const void *logits, int dtype, int64_t row_stride,
     hipStream_t stream = nullptr;
     int rc = mz_internal_launch_info(b, &B, &A, &stream);
     if (rc) return rc;
+    if (A > kWave)  // (one lane per action; the tree itself takes up to 255 actions)
+        return mz_internal_fail(MZ_ERR_UNSUPPORTED, "mz_root_glue: action_space_size > 64");
     if (!logits || !noises || !probs_out || !beta_out || !noises_out)
         return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: null buffer");
     if (dtype != MZ_DT_F32 && dtype != MZ_DT_F16) return mz_internal_fail(MZ_ERR_ARG, "mz_root_glue: bad dtype");
@@ -396,6 +400,8 @@ int mz_joint_action(mz_batch *b, const void *pred_logits, int dtype, int num_age
     hipStream_t stream = nullptr;
     int rc = mz_internal_launch_info(b, &B, &A, &stream);
     if (rc) return rc;
+    if (A > kWave)  // (one lane per action; the tree itself takes up to 255 actions)
+        return mz_internal_fail(MZ_ERR_UNSUPPORTED, "mz_joint_action: action_space_size > 64");
     if (num_agents < 1 || num_agents > kWave || current_agent < 0 || current_agent >= num_agents)
         return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: bad agent index / count");
     if (!actions || !joint_out) return mz_internal_fail(MZ_ERR_ARG, "mz_joint_action: null buffer");

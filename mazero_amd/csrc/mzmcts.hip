@@ -843,6 +843,117 @@ __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, in
 }
 
 // --------------------------------------------------------------------------------------------
+// CTree::expand (cnode.cpp:224-295), agent_num = 1, for action spaces past one lane per action
+// (64 < A <= kWideActions; k_prepare and k_hbm): lane l holds actions l + 64 j, j < 4.  The same
+// std::discrete_distribution restatement as expand_node -- the sequential double sum, p = w / sum,
+// the sequential prefix sums with the last forced to 1.0, two engine words per draw, lower_bound --
+// with the serial chains walking the chunks in action order.  pol / bet / noi: the node's A inputs
+// in global memory (noi may be null when eps == 0).
+// --------------------------------------------------------------------------------------------
+constexpr int kWideActions = 255;  // (Bn.y packs the action and the children count in 8 bits each)
+__device__ int expand_wide(const Geo &g, const Dev &d, int t, int parent, const float *pol_g, const float *bet_g,
+                           const float *noi_g, float eps, int K, float pv, int &cursor, int &tot, int &err,
+                           long long &st_new, int &wild, int *first_act = nullptr) {
+    const int l = lane_id();
+    const int A = g.A;
+    float pol[4], bet[4], noi[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int a = 64 * j + l;
+        pol[j] = (a < A) ? pol_g[a] : 0.f;
+        bet[j] = (a < A) ? bet_g[a] : 0.f;
+        noi[j] = (a < A && noi_g && eps > 0) ? noi_g[a] : 0.f;
+    }
+    int cnt[4] = {0, 0, 0, 0};  // draws that hit action 64 j + l
+    if (A < 2) {
+        cnt[0] = (l == 0) ? K : 0;
+    } else {
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double w = (double)bet[j];
+            for (int a = 0; a < kWave && 64 * j + a < A; ++a) sum += rld(w, a);
+        }
+        double cp[4];
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double p = (64 * j + l < A) ? (double)bet[j] / sum : 0.0;
+            double c = 0.0;
+            for (int a = 0; a < kWave && 64 * j + a < A; ++a) {
+                const double pa = rld(p, a);
+                acc = (j == 0 && a == 0) ? pa : acc + pa;
+                c = (l == a) ? acc : c;
+            }
+            if (64 * j + l == A - 1) c = 1.0;
+            cp[j] = c;
+        }
+        for (int k0 = 0; k0 < K; k0 += kWave) {
+            const int nk = (K - k0) < kWave ? (K - k0) : kWave;
+            double u = 0.0;
+            if (l < nk) {
+                const int w = cursor + 2 * (k0 + l);
+                const double w1 = (double)rng_word_lane(g, d, nullptr, 0, t, w, err);
+                const double w2 = (double)rng_word_lane(g, d, nullptr, 0, t, w + 1, err);
+                u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
+                if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
+            }
+            for (int k = 0; k < nk; ++k) {
+                const double uk = rld(u, k);
+                int idx = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) idx += __popcll(ballot(64 * j + l < A && cp[j] < uk));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) cnt[j] += (idx == 64 * j + l) ? 1 : 0;
+            }
+        }
+        cursor += 2 * K;
+    }
+    wait_vm();
+    unsigned long long m[4];
+    int below[4], nc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        m[j] = ballot(64 * j + l < A && cnt[j] > 0);
+        below[j] = nc;
+        nc += __popcll(m[j]);
+    }
+    if (first_act) {
+        int f = 0;
+#pragma unroll
+        for (int j = 3; j >= 0; --j)
+            if (m[j]) f = 64 * j + (int)__builtin_ctzll(m[j]);
+        *first_act = f;
+    }
+    if (tot + nc > g.P) {
+        err |= kErrPool;
+        return 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (cnt[j] > 0 && 64 * j + l < A) {
+            const int c = tot + below[j] + __popcll(m[j] & ((1ull << l) - 1ull));
+            const float bh = (float)cnt[j] / (float)K;  // betahat_prob = count / sampled_times
+            float prior = (eps > 0) ? (pol[j] * (1 - eps) + noi[j] * eps) : pol[j];
+            prior = prior * bh / bet[j];  // prior * betahat_prob / beta_prob
+            if (!tame_prior(prior)) wild = 1;
+            const size_t gi = (size_t)t * g.P + c;
+            d.A()[gi] = make_int4(0, f2i(prior), f2i(0.0f), f2i(0.0f));
+            d.Bn()[gi] = make_int4(0, pack_y(0, 64 * j + l, -1), f2i(0.0f), -1);
+            d.C()[gi] = make_float4(0.f, 0.f, 0.f, 0.f);
+            d.D()[gi] = make_float4(pol[j], bet[j], bh, 0.f);
+            d.Q()[gi] = 0.f;
+            d.PP()[gi] = pv;
+            d.Par()[gi] = parent;
+        }
+    }
+    wild = (ballot(wild != 0) != 0ull) ? 1 : 0;
+    st_new += nc;
+    tot += nc;
+    return nc;
+}
+
+// --------------------------------------------------------------------------------------------
 // CTree::expand (cnode.cpp:224-295) with agent_num = N > 1, K <= 64 (lane k = draw k).  One
 // discrete distribution per agent; draw k takes agent 0..N-1 in turn, two engine words per agent
 // draw (none when A < 2); key = key * 23333 + a_i in 64-bit two's complement (the reference's
@@ -1109,6 +1220,10 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         cur = nxt;
         nxt = tmp;
     }
+    // a root expansion that reads engine words past the LDS window (more than kRngWin / 2 engine-word
+    // pairs, or the wide expansion, which reads them all from HBM) reads what every wave just stored:
+    // a full workgroup barrier (stores drained) first
+    if (g.A > kMaxActions || 2 * a.K * g.N > kRngWin) __syncthreads();
     if (tid >= kWave) return;
 
     // ---- root expansion by wave 0 ----
@@ -1137,6 +1252,10 @@ __global__ __launch_bounds__(256) void k_prepare(const Params *__restrict__ prm,
         wait_lds();
         nc = expand_joint(g, d, t, 0, jp, jb, jn, a.eps, a.K, v, cursor, tot, w0, 0, nullptr, nullptr, jcp, jd, err,
                           st_new);
+    } else if (A > kMaxActions) {  // more actions than lanes (the root's inputs read from HBM)
+        const size_t ib = (size_t)t * A;
+        nc = expand_wide(g, d, t, 0, a.policy + ib, a.beta + ib, a.noise ? a.noise + ib : nullptr, a.eps, a.K, v,
+                         cursor, tot, err, st_new, wild, &first_act);
     } else {
         const size_t ib = (size_t)t * A;
         const float pol = (l < A) ? a.policy[ib + l] : 0.f;
@@ -5395,6 +5514,55 @@ __global__ __launch_bounds__(64) void k_gather(const char *pool, long long strid
     }
 }
 
+// The readback of a tree whose root may have more than 64 children or whose action space is
+// wider than a wave (64 < A <= kWideActions, agent_num = 1): the per-child fields 64 at a time, the
+// marginals through an action -> child map in LDS (with one agent a cell collects at most one child:
+// its visits, and 0 + its prior, as readback_emit's sums in child order give).
+__device__ void readback_wide(const RbPtrs &o, const Dev &d, size_t nb, float disc, int Wd, int t, int A, int nc,
+                              int fc, int4 ra, int *inv) {
+    const int l = lane_id();
+    if (l == 0) {
+        if (o.values) o.values[t] = (nc > 0) ? i2f(ra.z) : 0.f;
+        if (o.deg) o.deg[t] = nc;
+    }
+    for (int a = l; a < A; a += kWave) inv[a] = -1;
+    wait_lds();
+    for (int i = l; i < nc; i += kWave) inv[act_of(d.Bn()[nb + fc + i].y)] = i;
+    wait_lds();
+    if (o.mv || o.mp)
+        for (int a = l; a < A; a += kWave) {
+            const int i = inv[a];
+            int mv = 0;
+            float mp = 0.f;
+            if (i >= 0) {
+                const int4 ca = d.A()[nb + fc + i];
+                mv += ca.x;
+                mp += i2f(ca.y);
+            }
+            if (o.mv) o.mv[(size_t)t * A + a] = mv;
+            if (o.mp) o.mp[(size_t)t * A + a] = mp;
+        }
+    for (int i = l; i < Wd; i += kWave) {
+        const bool has = i < nc;
+        int4 ca = make_int4(0, 0, 0, 0), cb = ca;
+        float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (has) {
+            ca = d.A()[nb + fc + i];
+            cb = d.Bn()[nb + fc + i];
+            cd = d.D()[nb + fc + i];
+        }
+        const size_t r = (size_t)t * Wd + i;
+        const float val = i2f(ca.z), rew = i2f(ca.w);
+        if (int *fa = o.f[MZ_F_ACTIONS]) fa[r] = has ? act_of(cb.y) : 0;
+        if (o.f[MZ_F_VISIT_COUNT]) o.f[MZ_F_VISIT_COUNT][r] = has ? ca.x : 0;
+        const float fv[MZ_F_COUNT] = {0.f, 0.f, cd.x, cd.y, cd.z, i2f(ca.y), cd.z / cd.y * cd.x, i2f(cb.z), val, rew,
+                                      rew + disc * val};
+#pragma unroll
+        for (int f = MZ_F_PRED_PROBS; f < MZ_F_COUNT; ++f)
+            if (o.f[f]) ((float *)o.f[f])[r] = has ? fv[f] : 0.f;
+    }
+}
+
 // Readbacks (cnode.cpp:672-781 over CNode getters 69-171), all fields in one pass (readback_emit)
 __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm, float disc, int Wd, RbPtrs o) {
     const Geo g = prm->g;
@@ -5409,6 +5577,11 @@ __global__ __launch_bounds__(64) void k_readback(const Params *__restrict__ prm,
     {
         const int herr = d.hdr()[t].err;  // dead trees re-report their error (see k_prepare)
         if (l == 0 && herr) atomicOr(d.err(), herr);
+    }
+    if (g.N == 1 && (g.A > kMaxActions || Wd > kWave)) {
+        __shared__ int inv[kWideActions + 1];
+        readback_wide(o, d, nb, disc, Wd, t, g.A, nc, fc, ra, inv);
+        return;
     }
     int4 ca = make_int4(0, 0, 0, 0), cb = make_int4(0, 0, 0, 0);
     float4 cd = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -6203,12 +6376,15 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     if (B < 1 || A < 1 || K < 1 || S < 0) return fail(MZ_ERR_ARG, "bad tree-batch dimensions");
     if (B >= (1 << 24)) return fail(MZ_ERR_UNSUPPORTED, "root_num >= 2^24");  // packed with A in k_step's arguments
     if (N < 1) return fail(MZ_ERR_ARG, "agent_num must be >= 1");
-    if (A > kMaxActions) return fail(MZ_ERR_UNSUPPORTED, "action_space_size > 64");
-    if (N > 1 && (K > kWave || N > kWave || (long long)N * A > 4096))
+    // action spaces past one lane per action (64 < A <= 255) take the wide expansion and k_hbm;
+    // Bn.y packs the action and the children count in 8 bits each
+    if (A > kWideActions) return fail(MZ_ERR_UNSUPPORTED, "action_space_size > 255");
+    if (N > 1 && (K > kWave || N > kWave || A > kMaxActions || (long long)N * A > 4096))
         return fail(MZ_ERR_UNSUPPORTED, "joint-action trees (agent_num > 1) need sampled_times <= 64, "
-                                         "agent_num <= 64 and agent_num * action_space_size <= 4096");
+                                         "agent_num <= 64, action_space_size <= 64 and "
+                                         "agent_num * action_space_size <= 4096");
     if (S > 65000) return fail(MZ_ERR_UNSUPPORTED, "simulation_num > 65000");
-    if (K > 4096) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 4096");
+    if (K > (1 << 20)) return fail(MZ_ERR_UNSUPPORTED, "sampled_times > 2^20");
     // max degree of any node: min(K, A^N) (children are the distinct sampled joint actions,
     // cnode.cpp:242-294)
     int Wd = 1;
@@ -6241,7 +6417,12 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     // (leaf depth) words per selection, sum_{s<=S} (s+1); rounded up to whole 624-word blocks.
     {
         const long long need = 2ll * K * N * (S + 2) + (long long)(S + 1) * (S + 2) / 2 + kRngWin;
-        b->W = (int)(((need + kMtN - 1) / kMtN) * kMtN);
+        const long long w = ((need + kMtN - 1) / kMtN) * kMtN;
+        if (w > 0x7fffffffll) {
+            delete b;
+            return fail(MZ_ERR_UNSUPPORTED, "engine stream of a tree >= 2^31 words (sampled_times * simulation_num)");
+        }
+        b->W = (int)w;
     }
     if (hipGetDevice(&b->device) != hipSuccess) {
         delete b;
@@ -6343,7 +6524,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     // a pool whose LDS image does not fit one CU (or MZ_HBM=1 at mz_create, for tests): every step
     // launch of the handle is k_hbm, which keeps the tree in the arena (the reference allocates
     // K * (S + 2) nodes for any K and S, cnode.cpp:553-577)
-    b->hbm = g.lds > 160 * 1024 || getenv_flag("MZ_HBM");
+    b->hbm = g.lds > 160 * 1024 || A > kMaxActions || K > 4096 || getenv_flag("MZ_HBM");
     if (b->hbm) b->nc = 0;
     if (!b->hbm && K == 1 && N == 1 && !getenv_flag("MZ_NO_CHAIN")) {
         b->chain_nc = 0;

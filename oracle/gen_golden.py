@@ -59,6 +59,9 @@ CONFIGS = {
     # pools whose LDS image exceeds a CU's 160 KB (round 5: k_hbm; refused at construction before)
     "big_a64_k70_s60": (3, 64, 70, 60, 0.25, 0.3, False, {}),
     "big_27m_k16_s200": (2, 36, 16, 200, 0.25, 0.0, False, {}),
+    # action spaces past one lane per action (round 5: expand_wide, k_hbm; refused before)
+    "wide_a100_k5": (4, 100, 5, 40, 0.25, 0.3, False, {}),
+    "wide_a255_k300": (2, 255, 300, 12, 0.25, 0.0, False, {}),
 }
 
 

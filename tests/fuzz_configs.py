@@ -7,11 +7,12 @@ import numpy as np
 
 
 def fuzz_configs(seed: int, n: int):
-    """Seeded random small configurations across the kernels' classes and the search knobs."""
+    """Seeded random small configurations across the kernels' classes and the search knobs (A up to
+    255: past 64 actions the wide expansion and k_hbm)."""
     rng = np.random.default_rng(seed)
     out = []
     for _ in range(n):
-        A = int(rng.choice([1, 2, 3, 5, 9, 11, 15, 16, 17, 36, 63, 64]))
+        A = int(rng.choice([1, 2, 3, 5, 9, 11, 15, 16, 17, 36, 63, 64, 65, 130, 255]))
         K = int(rng.choice([1, 1, 2, 3, 5, 8, 10, 33, 64, 70]))
         S = int(rng.integers(1, 61))
         B = int(rng.integers(1, 49))
@@ -31,7 +32,7 @@ def fuzz_configs_large(seed: int, n: int):
     rng = np.random.default_rng(seed)
     out = []
     for _ in range(n):
-        A = int(rng.choice([5, 9, 11, 14, 17, 36, 64]))
+        A = int(rng.choice([5, 9, 11, 14, 17, 36, 64, 100]))
         K = int(rng.choice([1, 1, 2, 3, 5, 8, 10, 16]))
         S = int(rng.integers(60, 301))
         B = int(rng.integers(64, 513))

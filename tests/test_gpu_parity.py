@@ -229,6 +229,9 @@ BIG = [
     ("hbm_a64_k70_s60", 32, 64, 70, 60, 0.3),      # 3,905 reachable nodes
     ("hbm_27m_k16_s200", 64, 36, 16, 200, 0.0),    # 3,217
     ("hbm_k1_s2300", 2, 9, 1, 2300, 0.0),          # a K = 1 chain of 2,302 nodes (path records past 64 levels)
+    # action spaces past one lane per action (round 5: expand_wide + k_hbm; the reference has no bound)
+    ("wide_a100_k10", 64, 100, 10, 50, 0.3),
+    ("wide_a255_k300", 8, 255, 300, 20, 0.0),      # roots with > 64 children: chunked walk and readback
 ]
 
 
@@ -237,7 +240,8 @@ BIG_KERNEL = {"3m_k1": "k_chain3<64>", "27m_k1": "k_chain3<256>", "k1_chain512":
               "k1_chain1024": "k_chain<1024>", "k1_chain_general": "k_chain<0>",
               "27m_k8_general_layout": "k_step<0>", "k2_long_value_sets": "k_step<1024>",
               "k10_s200_general": "k_step<0>", "27m_k10_s200": "k_step<0>", "hbm_a64_k70_s60": "k_hbm",
-              "hbm_27m_k16_s200": "k_hbm", "hbm_k1_s2300": "k_hbm"}
+              "hbm_27m_k16_s200": "k_hbm", "hbm_k1_s2300": "k_hbm", "wide_a100_k10": "k_hbm",
+              "wide_a255_k300": "k_hbm"}
 
 
 @pytest.mark.parametrize("name,B,A,K,S,lz", BIG, ids=[b[0] for b in BIG])
@@ -260,6 +264,8 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert (out["marginal_visit_count"].sum(axis=(1, 2)) == S).all()
     deg = out["degree"]
     assert (deg >= 1).all() and (deg <= min(K, A)).all()
+    if name == "wide_a255_k300":
+        assert deg.max() > 64  # (the chunked paths ran)
     bh = out["sampled_beta_hat"].sum(axis=1)
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
 
@@ -527,6 +533,28 @@ def test_rebind_with_staged_expansion_after_stream_destroyed(gpu_lib, port_lib):
     out.update(readbacks(tb, g))
     exp.pop("sel_act")
     assert_same(out, exp, "gpu rebind (staged) ")
+
+
+def test_wide_action_space_limits(gpu_lib):
+    """Past 64 actions the tree takes up to 255 (Bn packs the action in 8 bits); the device driver
+    glue, one lane per action, refuses them with an error instead of computing garbage."""
+    import ctypes as C
+
+    from mazero_amd._capi import MZError
+    from mazero_amd.cytree import Tree_batch
+
+    with pytest.raises(MZError, match="255"):
+        Tree_batch(4, 1, 256, 5, 10, 0.01, 1, 0.75, 0.8, lib=gpu_lib)
+    with pytest.raises(MZError, match="joint"):
+        Tree_batch(4, 2, 65, 5, 10, 0.01, 1, 0.75, 0.8, lib=gpu_lib)
+    tb = Tree_batch(4, 1, 100, 5, 10, 0.01, 1, 0.75, 0.8, lib=gpu_lib)
+    assert tb.fused_kernel() == "k_hbm"
+    logits = torch.zeros(4, 1, 100, device="cuda")
+    probs = torch.empty(4, 100, device="cuda")
+    tb._sync_stream()
+    rc = gpu_lib.mz_policy_glue(tb._h, C.c_void_p(logits.data_ptr()), 0, 100, 0, 1.0, C.c_void_p(probs.data_ptr()),
+                                C.c_void_p(probs.data_ptr()))
+    assert rc != 0 and b"action_space_size > 64" in gpu_lib.mz_last_error()
 
 
 def test_too_many_simulations_raise(gpu_lib):
