@@ -3915,15 +3915,51 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
 #ifndef MZ_TREE_BK512
 #define MZ_TREE_BK512 MZ_TREE_BK
 #endif
+// The 1024-node class for searches with S + 1 <= 128 (round 5): 128-entry value-entry slots and
+// the layout below fit ~80 KB, two workgroups per CU (3s5z at K = 10: 512 trees of 1,011 nodes in
+// one round over the 256 CUs instead of two).  A class id of its own, one node above 1024.
+constexpr int kTree1024S = 1025;
 template <int NC>
 constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : (NC >= 1024 ? MZ_TREE_BK1024 : MZ_TREE_BK512);
 template <int NC>
 constexpr int kTreeWavesN = kBkN<NC> + 1;
 constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
 // the 512-node class with seven back-propagation waves keeps two workgroups per CU (76 KB of LDS
-// each) with slots of 128 entries (S + 1 <= 128; larger searches take k_step)
+// each) with slots of 128 entries (S + 1 <= 128; larger searches take k_step); so does kTree1024S
 template <int NC>
-constexpr int kBkCapN = (NC == 512 && kBkN<NC> > 4) ? 128 : kBkCap;
+constexpr int kBkCapN = (NC == kTree1024S || (NC == 512 && kBkN<NC> > 4)) ? 128 : kBkCap;
+// The 1024-node classes walk level by level instead (O(depth) after the barrier instead of
+// O(pool) / 4 waves).  Measured on one box, k_tree fused launch: 27m K = 5 (1010 nodes) 13.8 us by
+// levels against 14.1 us with tree_select_prep; 3m K = 5 (260 nodes) 10.4 against 11.6 us,
+// 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
+#ifndef MZ_LEVELS_FROM  // (experiment builds: the smallest class that walks by levels)
+#define MZ_LEVELS_FROM 1024
+#endif
+template <int NC>
+constexpr bool kTreeLevels = (NC >= MZ_LEVELS_FROM);
+// pb_c of the prior scores from the host table in HBM (one gather per node, L2-resident) instead of
+// the staged per-n factors and a double division per node: the gather's wait leaves the SIMD to the
+// wave that shares it.  Same-box A/B: 3s5z K = 5 10.50 -> 10.38 us, 3m K = 5 unchanged;
+// MZ_PBC_FACTORS builds the factor path for A/B runs
+#ifdef MZ_PBC_FACTORS
+template <int NC>
+constexpr bool kTreePbTable = kTreeLevels<NC>;
+#else
+template <int NC>
+constexpr bool kTreePbTable = true;
+#endif
+// The path nodes' new {value, reward} (sAz): per node where the precomputed walk's tie-list records
+// share the array, per path level in the level-walk classes (their walk knows which child lies on
+// the back-propagated path without a lookup: 8 B per node of LDS saved)
+template <int NC>
+constexpr bool kTreeAzLevel = kTreeLevels<NC>;
+// the value-set scalars staged for every node (MZ_C_STAGE A/B builds) or scalar-loaded per path
+// level (default, round 4; see bk_prestage)
+#ifdef MZ_C_STAGE
+constexpr bool kTreeCStage = true;
+#else
+constexpr bool kTreeCStage = false;
+#endif
 // per back-propagation wave, exchanged at barrier (2): its min/max partial, visited-node count,
 // error word and value-entry counters
 struct BkOut {
@@ -3936,8 +3972,12 @@ template <int NC>
 struct TreeLayout {
     static constexpr int r16(int x) { return (x + 15) & ~15; }
     static constexpr int BK = kBkN<NC>;
-    static constexpr int kTreeReg = (2 * BK * kBkCapN<NC> > kRegCap) ? 2 * BK * kBkCapN<NC> : kRegCap;  // staging int2s
-    static constexpr int PSx = NC / 2 + 1;                         // PS = S + 2 <= P / K <= NC / 2
+    static constexpr int CAP = kBkCapN<NC>;
+    // staging int2s: two slots per back-propagation wave, at least 16 KiB for big leaf rows except in
+    // kTree1024S (its rows up to 8 * kTreeReg bytes are staged, larger ones copied directly)
+    static constexpr int kTreeReg = (NC == kTree1024S || 2 * BK * CAP > kRegCap) ? 2 * BK * CAP : kRegCap;
+    // path levels: PS = S + 2 <= P / K <= NC / 2, and S + 1 <= CAP (the handle takes k_tree only then)
+    static constexpr int PSx = (NC / 2 + 1 < CAP + 1) ? NC / 2 + 1 : CAP + 1;
     static constexpr int oA = 0;                                   // int4 [NC] staged {visit, prior, value, reward}
     static constexpr int oB = oA + r16(16 * NC);                   // int4 [NC] staged structure records
     static constexpr int oPP = oB + r16(16 * NC);                  // f32 [NC] parent's pred_value
@@ -3945,8 +3985,9 @@ struct TreeLayout {
     static constexpr int oPar = oQ + r16(4 * NC);                  // i32 [NC] parent index
     static constexpr int oPS = oPar + r16(4 * NC);                 // f32 [NC] prior score after the back-propagation
     static constexpr int oFl = oPS + r16(4 * NC);                  // i32 [NC] 1 + path level (path nodes), else 0
-    static constexpr int oAz = oFl + r16(4 * NC);                  // float2 [NC] path nodes' new {value, reward}
-    static constexpr int oPath = oAz + r16(8 * NC);                // int2 [PSx] the path {node, visits at selection}
+    static constexpr int oAz = oFl + r16(4 * NC);                  // float2 path nodes' new {value, reward}
+    // (per node [NC], or per path level [PSx + 64] in the level-walk classes, kTreeAzLevel)
+    static constexpr int oPath = oAz + (kTreeAzLevel<NC> ? r16(8 * (PSx + kWave)) : r16(8 * NC));  // int2 [PSx] the path
     static constexpr int oLp = oPath + r16(8 * (PSx + kWave));     // f32 lambda powers
     static constexpr int oRng = oLp + r16(4 * (PSx + 1 + kWave));  // u32 [kRngWin] engine words
     static constexpr int oBoot = oRng + r16(4 * kRngWin);          // f32 [BK][PSx + 64] bootstrap values
@@ -3959,10 +4000,10 @@ struct TreeLayout {
     static constexpr int oPol = oIx + r16(4 * kWave);              // f32 [64] the leaf's policy
     static constexpr int oNxt = oPol + r16(4 * kWave);             // u32 [64] the header's engine words
     static constexpr int oSt = oNxt + r16(4 * kWave);              // i64 [64] the tree's statistics counters
-    static constexpr int oCn = oSt + r16(8 * kWave);               // float4 [NC] staged value-set scalars
-    static constexpr int oPb = oCn + r16(16 * NC);                 // f32 [PSx] logf((n + c2 + 1)/c2) + c1
-    static constexpr int oSq = oPb + r16(4 * (PSx + kWave));       // f64 [PSx] sqrt(n)
-    static constexpr int oXB = oSq + r16(8 * (PSx + kWave));        // BkOut [BK + 1] (index = wave)
+    static constexpr int oCn = oSt + r16(8 * kWave);               // float4 [NC] staged value-set scalars (kTreeCStage)
+    static constexpr int oPb = oCn + (kTreeCStage ? r16(16 * NC) : 0);  // f32 [PSx] logf((n + c2 + 1)/c2) + c1
+    static constexpr int oSq = oPb + (kTreePbTable<NC> ? 0 : r16(4 * (PSx + kWave)));  // f64 [PSx] sqrt(n)
+    static constexpr int oXB = oSq + (kTreePbTable<NC> ? 0 : r16(8 * (PSx + kWave)));  // BkOut [BK + 1] (index = wave)
     static constexpr int total = oXB + r16((int)sizeof(BkOut) * (BK + 1));
 };
 int tree_lds_bytes(int nc) {
@@ -3972,9 +4013,11 @@ int tree_lds_bytes(int nc) {
         case 256: return TreeLayout<256>::total;
         case 384: return TreeLayout<384>::total;
         case 512: return TreeLayout<512>::total;
+        case kTree1024S: return TreeLayout<kTree1024S>::total;
         default: return TreeLayout<1024>::total;
     }
 }
+static_assert(TreeLayout<kTree1024S>::total <= 80 * 1024, "kTree1024S: two workgroups per CU");
 
 // ------------------------------------------------------------------------------------------------
 // k_tree's back-propagation on four waves: path level i belongs to wave 1 + i % 4 (kBk waves).
@@ -3991,11 +4034,7 @@ int tree_lds_bytes(int nc) {
 // (the pre-staged levels' in round 1, from the path records it already holds; later levels when it
 // reaches them), instead of a round-1 LDS-DMA of every node's record (16 bytes x the pool per tree
 // and launch, round 3).  MZ_C_STAGE builds the staged variant for A/B runs.
-#ifdef MZ_C_STAGE
-constexpr bool kTreeCStage = true;
-#else
-constexpr bool kTreeCStage = false;
-#endif
+// (kTreeCStage: defined with the class traits above)
 
 struct BkPre {
     int n0, nv0, n1, nv1;  // the pre-staged levels' nodes and entry counts (nv < 0: not staged)
@@ -4100,7 +4139,7 @@ __device__ __forceinline__ void bk_boot(const Lds &s, float *boot, int D, float 
 }
 
 // wave k's path levels k, k + BK, ... (CTree::back_propagate, cnode.cpp:415-450, node by node)
-template <int BK, int CAP>
+template <int BK, int CAP, bool AZL>  // AZL: sAz per path level (kTreeAzLevel), else per node
 __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds &s, const float4 *sCn, float2 *sAz,
                                           const float *boot, int2 *sReg, BkPre pre, int t, int D, float reward,
                                           float disc, int k, int &err, long long &ent_r, long long &ent_w, float &pmn,
@@ -4220,7 +4259,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
             d.C()[gi] = make_float4(ws, tw, 0.f, 0.f);
             if (!is_leaf && dep > md_of(by)) d.Bn()[gi] = make_int4(b4.x, pack_y(nc, act_of(by), dep), b4.z, b4.w);
             if (i >= 1) d.Q()[gi] = q;
-            sAz[n] = make_float2(val, i2f(a4.w));
+            sAz[AZL ? i : n] = make_float2(val, i2f(a4.w));
         }
         if (i >= 1) {
             pmn = fminf(pmn, q);
@@ -4242,27 +4281,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
 // Wave 0 then chases next nodes one LDS read per level.
 constexpr int kTreeLeaf = -1, kTreeSlow = -2;
 
-// The 1024-node class walks level by level instead (O(depth) after the barrier instead of
-// O(pool) / 4 waves).  Measured on one box, k_tree fused launch: 27m K = 5 (1010 nodes) 13.8 us by
-// levels against 14.1 us with tree_select_prep; 3m K = 5 (260 nodes) 10.4 against 11.6 us,
-// 3s5z K = 5 (510 nodes) 12.0 against 12.6 us the other way round.
-#ifndef MZ_LEVELS_FROM  // (experiment builds: the smallest class that walks by levels)
-#define MZ_LEVELS_FROM 1024
-#endif
-template <int NC>
-constexpr bool kTreeLevels = (NC >= MZ_LEVELS_FROM);
 
-// pb_c of the prior scores from the host table in HBM (one gather per node, L2-resident) instead of
-// the staged per-n factors and a double division per node: the gather's wait leaves the SIMD to the
-// wave that shares it.  Same-box A/B: 3s5z K = 5 10.50 -> 10.38 us, 3m K = 5 unchanged;
-// MZ_PBC_FACTORS builds the factor path for A/B runs
-#ifdef MZ_PBC_FACTORS
-template <int NC>
-constexpr bool kTreePbTable = kTreeLevels<NC>;
-#else
-template <int NC>
-constexpr bool kTreePbTable = true;
-#endif
 
 // Who stages the value-set scalars in round 1: wave 0 (with the path, the flags and the leaf's
 // inputs) or, for the 1024-node class, wave 4.  Same-box A/B: 3m K = 10 9.77 -> 9.64 us with wave 4;
@@ -4395,6 +4414,31 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
         const float delta = mmx - mmn;
         den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
     }
+#ifndef MZ_S12_SPLIT
+    // (S) one pass, round 5: every internal node scores its own children inline (ucb_score,
+    // cnode.cpp:297-335: the prior score of waves 2 .. kBk plus the min/max-normalised value score)
+    // and resolves select_child (cnode.cpp:337-379).  Each non-root node is the child of exactly one
+    // internal node, so every score is computed once, with round 4's operations; the pass needs no
+    // barrier between the scores and the tie lists.  The exact records' list bits go to the
+    // value-entry staging area (free after barrier (2)): sAz, which the scores read, stays intact.
+    float2 *sRec = (float2 *)(smem + L::oReg);
+    auto score = [&](int c) {
+        const int4 a = sA[c];
+        const int fl = sFl[c];
+        const float2 az = sAz[c];
+        const int vis = a.x + (fl ? 1 : 0);
+        const float val = fl ? az.x : i2f(a.z);
+        const float rw = fl ? az.y : i2f(a.w);
+        float vs = (vis == 0) ? 0.0f : ((rw + disc * val) - sPP[c]);
+        if (mm_on) vs = (vs - mmn) / den;
+        if (vs < 0) vs = 0;
+        if (vs > 1) vs = 1;
+        return sSc[c] + vs;  // prior_score + value_score
+    };
+    if (MZ_STAMPS && tp) tp[0] = __builtin_amdgcn_s_memtime();
+#else
+    float2 *sRec = sAz;
+    auto score = [&](int c) { return sSc[c]; };
     for (int n0 = wv * kWave; n0 < ntot; n0 += 4 * kWave) {  // (S1)
         const int n = n0 + l;
         if (n >= 1 && n < ntot) {
@@ -4416,6 +4460,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
         tp[0] = __builtin_amdgcn_s_memtime();
     }
     lds_barrier();  // (3)
+#endif
     for (int p0 = wv * kWave; p0 < ntot; p0 += 4 * kWave) {  // (S2)
         const int p = p0 + l;
         if (p < ntot) {
@@ -4437,7 +4482,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
                     // the sign of a zero maximum irrelevant
                     float sc[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) sc[u] = sSc[fc + (u < nc ? u : 0)];
+                    for (int u = 0; u < 8; ++u) sc[u] = score(fc + (u < nc ? u : 0));
 #pragma unroll
                     for (int u = 0; u < 8; ++u)
                         if (u >= nc) sc[u] = -INFINITY;
@@ -4463,7 +4508,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
                 for (int i0 = 0; i0 < nc; i0 += 4) {
                     float sc[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) sc[u] = sSc[fc + ((i0 + u < nc) ? i0 + u : i0)];
+                    for (int u = 0; u < 4; ++u) sc[u] = score(fc + ((i0 + u < nc) ? i0 + u : i0));
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int i = i0 + u;
@@ -4481,7 +4526,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
                     nxt[p] = fc + __builtin_ctzll(lst);
                 } else {
                     nxt[p] = kTreeSlow;
-                    sAz[p] = make_float2(i2f((int)(unsigned)(lst & 0xffffffffull)), i2f((int)(unsigned)(lst >> 32)));
+                    sRec[p] = make_float2(i2f((int)(unsigned)(lst & 0xffffffffull)), i2f((int)(unsigned)(lst >> 32)));
                     sQ[p] = i2f(cnt | (terr ? 0x10000 : 0));
                 }
             }
@@ -4509,7 +4554,11 @@ __device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, in
     int2 *sPath = (int2 *)(smem + L::oPath);
     const unsigned *sRng = (const unsigned *)(smem + L::oRng);
     const int *nxt = (const int *)(smem + L::oPar);
+#ifndef MZ_S12_SPLIT
+    const float2 *rec = (const float2 *)(smem + L::oReg);  // (tree_select_prep's exact records)
+#else
     const float2 *rec = (const float2 *)(smem + L::oAz);
+#endif
     cursor = uni(cursor);
     int v;
     const unsigned nxb = lds_addr(smem) + L::oPar;
@@ -4746,7 +4795,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         int berr = 0;
         long long ber = 0, bew = 0;
         float bmn, bmx;
-        bk_levels<BK, kBkCapN<NC>>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+        bk_levels<BK, kBkCapN<NC>, kTreeAzLevel<NC>>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, wv - 1, berr, ber, bew, bmn, bmx);
         stamp(ts, 3);
         // nodes 1 .. tot-1 in 64-node blocks dealt round-robin over waves 2 .. kBk, the deepest
@@ -4875,7 +4924,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         int err = 0;
         long long ent_r = 0, ent_w = 0;
         float pmn, pmx;
-        bk_levels<BK, kBkCapN<NC>>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
+        bk_levels<BK, kBkCapN<NC>, kTreeAzLevel<NC>>(g, d, s, (const float4 *)(smem + L::oCn), sAz, boot, (int2 *)(smem + L::oReg), pre, t, D, r_in,
                   discount, 0, err, ent_r, ent_w, pmn, pmx, tl);
         if (l == 0) {
             xbo[1].mn = pmn;
@@ -4975,6 +5024,10 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     d.o_D = pl->d.o_D;
     d.o_R = pl->d.o_R;
     const int wbase = h.cursor;
+    // pb_c(0, 0) pinned to an SGPR here, with the header's scalar round trip: left to the compiler the
+    // load sank to its use in the expansion as a vector load, whose wait (vmcnt(0)) also waited for
+    // the new children's stores there and left a vmcnt(0) in the score pass behind it
+    asm volatile("" ::"s"(t00));
     // the selection's engine words (the expansion's when K > kNxt / 2): word wbase + o is sRng[o + wsh].
     // One 16-byte chunk per lane from the aligned word below wbase when the window lies inside the
     // stream (the tree's stream starts 16-byte aligned: W is a multiple of 624), else four dword chunks.
@@ -5197,14 +5250,18 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             float cpp = 0.f, cps = 0.f;
             float2 caz = make_float2(0.f, 0.f);
             int cfl = 0;
+            // (per-level sAz: a child on the back-propagated path sits at level Dn + 1 of it, since the
+            // walk reaches the path's nodes at their own depths; read with the children's records)
+            const float2 azl = kTreeAzLevel<NC> ? sAz[Dn + 1] : make_float2(0.f, 0.f);
             if (has) {
                 ca = sA[fc + l];
                 cb = sB[fc + l];
                 cpp = sPP[fc + l];
                 cps = sPS[fc + l];
                 cfl = sFl[fc + l];
-                caz = sAz[fc + l];
+                if constexpr (!kTreeAzLevel<NC>) caz = sAz[fc + l];
             }
+            if constexpr (kTreeAzLevel<NC>) caz = azl;
             const int cvis = ca.x + (cfl ? 1 : 0);
             int ci = 0;
             if (x == 0 && xv <= nc) {
@@ -5316,7 +5373,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) &
                          15) == 0;
         const long long o = (long long)l * 16;
-        if (al && row_bytes <= 16 * 16 * kWave && row_bytes <= 8ll * kRegCap) {
+        if (al && row_bytes <= 16 * 16 * kWave && row_bytes <= 8ll * L::kTreeReg) {
             const long long last = row_bytes - 16;
             for (int k = 0; 1024ll * k < row_bytes; ++k)
                 glds16a(src + (o + 1024 * k < last ? o + 1024 * k : last), sbig + 1024 * k);
@@ -5392,8 +5449,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         if (rbd) {
             auto upd = [&](int n) {
                 int4 a = sA[n];
-                if (sFl[n]) {
-                    const float2 az = sAz[n];
+                const int fl = sFl[n];
+                if (fl) {
+                    const float2 az = sAz[kTreeAzLevel<NC> ? fl - 1 : n];
                     a = make_int4(a.x + 1, a.y, f2i(az.x), f2i(az.y));
                 }
                 return a;
@@ -6105,6 +6163,7 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
                 case 256: launch_tree<256>(b, a); break;
                 case 384: launch_tree<384>(b, a); break;
                 case 512: launch_tree<512>(b, a); break;
+                case kTree1024S: launch_tree<kTree1024S>(b, a); break;
                 default: launch_tree<1024>(b, a); break;
             }
         } else {
@@ -6114,6 +6173,7 @@ int launch_step(mz_batch *b, bool eb, bool sel, StepArgs a) {
                 case 256: launch_tree<256, false>(b, a); break;
                 case 384: launch_tree<384, false>(b, a); break;
                 case 512: launch_tree<512, false>(b, a); break;
+                case kTree1024S: launch_tree<kTree1024S, false>(b, a); break;
                 default: launch_tree<1024, false>(b, a); break;
             }
         }
@@ -6536,8 +6596,11 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         if (chain_lds_bytes(b->P, b->chain_nc) + 16 * 16 * kWave > 160 * 1024) b->chain_nc = -1;
     }
     // (k_tree stages one path node's value entries per slot: E <= kBkCap)
-    if (!b->hbm && N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE"))
+    if (!b->hbm && N == 1 && K >= 2 && K <= kWave && b->nc > 0 && g.E <= (b->nc == 512 ? kBkCapN<512> : kBkCap) && !getenv_flag("MZ_NO_TREE")) {
         b->tree_nc = b->nc;
+        // searches of S + 1 <= 128 in the 1024-node class: the ~80 KB layout, two workgroups per CU
+        if (b->nc == 1024 && g.E <= kBkCapN<kTree1024S> && !getenv_flag("MZ_NO_TREE_1024S")) b->tree_nc = kTree1024S;
+    }
     b->zc = !getenv_flag("MZ_HOST_COPY");
     b->fused_rb = !getenv_flag("MZ_NO_FUSED_READBACK");
     Dev &d = b->dev;
@@ -6652,6 +6715,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
             case 256: (void)hipFuncSetAttribute((const void *)k_tree<256, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<256, false>, attr, tl); break;
             case 384: (void)hipFuncSetAttribute((const void *)k_tree<384, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<384, false>, attr, tl); break;
             case 512: (void)hipFuncSetAttribute((const void *)k_tree<512, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<512, false>, attr, tl); break;
+            case kTree1024S: (void)hipFuncSetAttribute((const void *)k_tree<kTree1024S, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<kTree1024S, false>, attr, tl); break;
             default: (void)hipFuncSetAttribute((const void *)k_tree<1024, true>, attr, tl); (void)hipFuncSetAttribute((const void *)k_tree<1024, false>, attr, tl); break;
         }
     }
@@ -6967,6 +7031,7 @@ int mz_fused_kernel(mz_batch *b, char *out, int len) {
     if (b->hbm) std::snprintf(name, sizeof name, b->N > 1 ? "k_hbm<joint>" : "k_hbm");
     else if (b->chain3_nc > 0) std::snprintf(name, sizeof name, "k_chain3<%d>", b->chain3_nc);
     else if (b->chain_nc >= 0) std::snprintf(name, sizeof name, "k_chain<%d>", b->chain_nc);
+    else if (b->tree_nc == kTree1024S) std::snprintf(name, sizeof name, "k_tree<1024,s128>");
     else if (b->tree_nc > 0) std::snprintf(name, sizeof name, "k_tree<%d>", b->tree_nc);
     else if (b->N > 1) std::snprintf(name, sizeof name, "k_step<0,joint>");
     else std::snprintf(name, sizeof name, "k_step<%d>", b->nc);

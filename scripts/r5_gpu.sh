@@ -1,0 +1,44 @@
+#!/bin/bash
+# Round-5 box pass: STEPS="tests ab stamps bench" (default "tests"), each step under its own limit,
+# stopping at the first failing step.  Logs under gpurun_out/r5/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+O=gpurun_out/r5; mkdir -p $O
+STEPS=${STEPS:-tests}
+for st in $STEPS; do
+  case $st in
+    tests)
+      timeout -k 10 1050 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ${PYK:+-k "$PYK"} \
+        > $O/tests.log 2>&1; rc=$?; tail -15 $O/tests.log; [ $rc -ne 0 ] && exit $rc ;;
+    ab)
+      # interleaved A/B of the fused kernel (HIP-event mean per launch) against experiment builds
+      for rep in 1 2; do
+        for cfg in ${AB:-3m_k5 3m_k10 3s5z_k5 3s5z_k10 27m_k5}; do
+          case $cfg in
+            3m_k5) a="--sampled-times 5";; 3m_k10) a="--sampled-times 10";;
+            3s5z_k5) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5";;
+            3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
+            27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
+            3m_k1) a="--sampled-times 1";;
+          esac
+          line="$cfg rep$rep"
+          for v in prod ${ALTS:-r4 split}; do
+            if [ $v = prod ]; then env=""; elif [ $v = no1024s ]; then env="MZ_NO_TREE_1024S=1"; else env="MZ_LIB_OVERRIDE=$PWD/mazero_amd/_build/variant_$v.so"; fi
+            env $env timeout -k 10 200 python bench.py --no-cpu --steps 5 --warmup 2 $a > $O/ab_${cfg}_${v}_$rep.json 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
+            line="$line $v $(grep -o '"avg_launch_us": [0-9.]*' $O/ab_${cfg}_${v}_$rep.json | cut -d' ' -f2)/$(grep -o '"ms_per_step": [0-9.]*' $O/ab_${cfg}_${v}_$rep.json | head -1 | cut -d' ' -f2)"
+          done
+          echo "$line" | tee -a $O/ab.txt
+        done
+      done ;;
+    stamps)
+      for cfg in ${STAMPCFG:-3m_k5}; do
+        case $cfg in
+          3m_k5) a="--sampled-times 5";; 3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
+          27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
+        esac
+        MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a > $O/stamps_$cfg.json 2> $O/stamps.err || exit 1
+      done ;;
+    bench)
+      timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?; cat $O/bench.json; [ $rc -ne 0 ] && exit $rc ;;
+  esac
+done
