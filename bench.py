@@ -286,6 +286,15 @@ class HipLeg:
             avg_launch_us=round(avg * 1e6, 3),
             mean_path_len=round(st["path_edges"] / max(1, st["selects"]), 3),
         )
+        if "mm_moved" in st and K > 1:
+            # back-propagations after which the min/max normaliser moved (every internal node's
+            # select_child outcome can change then), per tree and per launch: a launch's duration is
+            # its slowest tree's, so the launch with no moved tree is what an incremental rescore needs
+            backups = max(1, st["expands"] - N * steps * B)  # (minus the prepares' root expansions)
+            p_move = st["mm_moved"] / backups
+            r["normaliser_moved_per_backup"] = round(p_move, 4)
+            r["launches_without_a_moved_tree"] = float(f"{(1.0 - p_move) ** B:.3e}")
+        return r
         if span is not None:
             r["launch_span"] = span
         if os.environ.get("MZ_STAMPS") == "1" and st.get("stamped", 0) > 0:

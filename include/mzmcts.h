@@ -75,32 +75,36 @@ enum mz_stat {
     MZ_S_ENTRIES_READ = 6,   /* value-set entries scanned by back-propagation              */
     MZ_S_ENTRIES_WRITTEN = 7,/* value-set entries written by back-propagation              */
     MZ_S_MINMAX_NODES = 8,   /* node q-values scanned for the min/max normaliser           */
+    MZ_S_MM_MOVED = 9,       /* back-propagations after which the min/max normaliser (its min
+                              * or max, CMinMaxStats utils.cpp:79-103) differs from before:
+                              * every internal node's select_child outcome may change then
+                              * (counted by k_tree, k_step and k_hbm; 0 for the K = 1 chains)  */
     /* Diagnostic builds only (compiled with MZ_STAMPS=1; zero otherwise): shader cycles of the
      * fused simulation-step kernel, summed over trees and launches, read with s_memtime where the
      * wave's instruction stream reaches each point (no forced waits).  Wave 0 (expansion,
      * selection, gather): */
-    MZ_S_CYC_HEADER = 9,     /* round 1: header, tables, network outputs issued and waited   */
-    MZ_S_CYC_STAGE1 = 10,    /* slow-path check (host bounds too small)                    */
-    MZ_S_CYC_STAGE2 = 11,    /* round 2 issue: RNG window, the leaf's record               */
-    MZ_S_CYC_EXPAND = 12,    /* leaf expansion                                             */
-    MZ_S_CYC_BACKUP = 13,    /* waiting for the back-propagation wave (barrier)            */
-    MZ_S_CYC_MINMAX = 14,    /* waiting for the RNG window                                 */
-    MZ_S_CYC_SELECT = 15,    /* value scores + selection walk                              */
-    MZ_S_CYC_GATHER = 16,    /* hidden-state gather loads                                  */
-    MZ_S_CYC_EPILOGUE = 17,  /* header write-back, gather stores, statistics               */
-    MZ_S_STAMPED = 18,       /* stamped launches x trees                                   */
+    MZ_S_CYC_HEADER = 10,     /* round 1: header, tables, network outputs issued and waited   */
+    MZ_S_CYC_STAGE1 = 11,    /* slow-path check (host bounds too small)                    */
+    MZ_S_CYC_STAGE2 = 12,    /* round 2 issue: RNG window, the leaf's record               */
+    MZ_S_CYC_EXPAND = 13,    /* leaf expansion                                             */
+    MZ_S_CYC_BACKUP = 14,    /* waiting for the back-propagation wave (barrier)            */
+    MZ_S_CYC_MINMAX = 15,    /* waiting for the RNG window                                 */
+    MZ_S_CYC_SELECT = 16,    /* value scores + selection walk                              */
+    MZ_S_CYC_GATHER = 17,    /* hidden-state gather loads                                  */
+    MZ_S_CYC_EPILOGUE = 18,  /* header write-back, gather stores, statistics               */
+    MZ_S_STAMPED = 19,       /* stamped launches x trees                                   */
     /* wave 1 (back-propagation): */
-    MZ_S_CYC_W1_ROUND1 = 19, /* round 1: node records, path, lambda powers issued and waited */
-    MZ_S_CYC_W1_STAGE2 = 20, /* round 2 issue: path-node value sets, value entries         */
-    MZ_S_CYC_W1_BACKUP = 21, /* back-propagation + min/max                                 */
-    MZ_S_CYC_W1_SYNC = 22,   /* wave 1's whole span, start to back-propagation done        */
-    MZ_S_CYC_EXP_CDF = 23,   /* expansion: sampling distribution                           */
-    MZ_S_CYC_EXP_DRAW = 24,  /* expansion: K draws                                         */
-    MZ_S_CYC_EXP_NODES = 25, /* expansion: child creation                                  */
-    MZ_S_CYC_BAK_BOOT = 26,  /* back-propagation: bootstrap values                         */
-    MZ_S_CYC_BAK_WAIT = 27,  /* back-propagation: waiting for staged entries               */
-    MZ_S_CYC_BAK_NODES = 28, /* back-propagation: node updates                             */
-    MZ_S_COUNT = 29
+    MZ_S_CYC_W1_ROUND1 = 20, /* round 1: node records, path, lambda powers issued and waited */
+    MZ_S_CYC_W1_STAGE2 = 21, /* round 2 issue: path-node value sets, value entries         */
+    MZ_S_CYC_W1_BACKUP = 22, /* back-propagation + min/max                                 */
+    MZ_S_CYC_W1_SYNC = 23,   /* wave 1's whole span, start to back-propagation done        */
+    MZ_S_CYC_EXP_CDF = 24,   /* expansion: sampling distribution                           */
+    MZ_S_CYC_EXP_DRAW = 25,  /* expansion: K draws                                         */
+    MZ_S_CYC_EXP_NODES = 26, /* expansion: child creation                                  */
+    MZ_S_CYC_BAK_BOOT = 27,  /* back-propagation: bootstrap values                         */
+    MZ_S_CYC_BAK_WAIT = 28,  /* back-propagation: waiting for staged entries               */
+    MZ_S_CYC_BAK_NODES = 29, /* back-propagation: node updates                             */
+    MZ_S_COUNT = 30
 };
 
 /* --- library -------------------------------------------------------------------------- */

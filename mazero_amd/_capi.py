@@ -50,6 +50,7 @@ STATS = [
     "entries_read",
     "entries_written",
     "minmax_nodes",
+    "mm_moved",
     "cyc_header",
     "cyc_stage1",
     "cyc_stage2",

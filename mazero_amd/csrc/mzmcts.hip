@@ -2532,10 +2532,14 @@ __global__ __launch_bounds__(128) void k_step(char *base, int P, int PS, int BA,
             const int *xi = (const int *)(xst + 2 * MZ_S_COUNT);
             // diagnostic builds: how much later than wave 0 wave 1 started (in the 'minmax' slot)
             if (MZ_STAMPS && SEL) stl[MZ_S_CYC_MINMAX] += xst[2 * MZ_S_COUNT + 2] - (long long)ts[0];
+            const float omn = h.mm_min, omx = h.mm_max;
+            const int ocnt = h.mm_cnt;
             h.mm_min = unif(xf[0]);
             h.mm_max = unif(xf[1]);
             h.mm_cnt = uni(xi[2]);
             err |= uni(xi[3]);
+            if (h.mm_cnt > 0 && (ocnt == 0 || f2i(h.mm_min) != f2i(omn) || f2i(h.mm_max) != f2i(omx)))
+                stl[MZ_S_MM_MOVED] += 1;
         }
         if (!err) {
             h.cursor = cursor;
@@ -4414,13 +4418,14 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
         const float delta = mmx - mmn;
         den = (gdelta < delta) ? delta : gdelta;  // std::max(delta_lb, delta)
     }
-#ifndef MZ_S12_SPLIT
-    // (S) one pass, round 5: every internal node scores its own children inline (ucb_score,
-    // cnode.cpp:297-335: the prior score of waves 2 .. kBk plus the min/max-normalised value score)
-    // and resolves select_child (cnode.cpp:337-379).  Each non-root node is the child of exactly one
-    // internal node, so every score is computed once, with round 4's operations; the pass needs no
-    // barrier between the scores and the tie lists.  The exact records' list bits go to the
-    // value-entry staging area (free after barrier (2)): sAz, which the scores read, stays intact.
+#ifdef MZ_S12_FUSED
+    // (S) one pass (round-5 experiment, MZ_S12_FUSED builds): every internal node scores its own
+    // children inline (ucb_score, cnode.cpp:297-335) and resolves select_child (cnode.cpp:337-379),
+    // with no barrier between the scores and the tie lists; the exact records' list bits go to the
+    // value-entry staging area.  Measured and kept out (same-box A/B, fused launch): 3m K = 5
+    // 7.57 -> 8.65 us, 3m K = 10 7.87 -> 9.71, 3s5z K = 5 10.25 -> 11.57: a lane scores up to eight
+    // children (~25 instructions each, every lane of the wave issuing them) where (S1) scores one
+    // node per lane, which costs more than the barrier it saves.
     float2 *sRec = (float2 *)(smem + L::oReg);
     auto score = [&](int c) {
         const int4 a = sA[c];
@@ -4554,7 +4559,7 @@ __device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, in
     int2 *sPath = (int2 *)(smem + L::oPath);
     const unsigned *sRng = (const unsigned *)(smem + L::oRng);
     const int *nxt = (const int *)(smem + L::oPar);
-#ifndef MZ_S12_SPLIT
+#ifdef MZ_S12_FUSED
     const float2 *rec = (const float2 *)(smem + L::oReg);  // (tree_select_prep's exact records)
 #else
     const float2 *rec = (const float2 *)(smem + L::oAz);
@@ -5019,6 +5024,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     h.err = hp0->err;
     h.tame = hp0->tame;
     h.leaf = hp0->leaf;
+    h.mm_min = hp0->mm_min;  // (the normaliser before this back-propagation: MZ_S_MM_MOVED)
+    h.mm_max = hp0->mm_max;
+    h.mm_cnt = hp0->mm_cnt;
     const int gW = pl->g.W;
     const float gdelta = pl->g.delta;
     d.o_D = pl->d.o_D;
@@ -5210,6 +5218,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     float mmn, mmx;
     int mm_cnt;
     bk_minmax<NC>(smem, D, mmn, mmx, mm_cnt);
+    const int moved = (mm_cnt > 0 && (h.mm_cnt == 0 || f2i(mmn) != f2i(h.mm_min) || f2i(mmx) != f2i(h.mm_max))) ? 1 : 0;
     long long ent_r = 0, ent_w = 0;
 #pragma unroll
     for (int j = 1; j <= BK; ++j) {
@@ -5491,6 +5500,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             case MZ_S_ENTRIES_READ: add = ent_r; break;
             case MZ_S_ENTRIES_WRITTEN: add = ent_w; break;
             case MZ_S_MINMAX_NODES: add = tot - 1; break;
+            case MZ_S_MM_MOVED: add = moved; break;
             case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;    // round 1
             case MZ_S_CYC_STAGE2: add = (long long)(ts[2] - ts[1]); break;    // barrier (1) wait
             case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;    // draws + children

@@ -38,6 +38,19 @@ for st in $STEPS; do
         esac
         MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a > $O/stamps_$cfg.json 2> $O/stamps.err || exit 1
       done ;;
+    segv)
+      # the round-3/4 profiler abort: the 27m K = 1 --pmc pass over the env step's graph (5,481 kernel
+      # nodes), with the fault's address, PC, thread and the process's mappings dumped by
+      # scripts/segv_maps.c; the same pass eagerly first (its mappings at exit).  Last step of a call.
+      a="--no-cpu --steps 1 --warmup 1 --map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1"
+      MZ_SEGV_MAPS=$PWD/$O/segv_eager.txt timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+        -d $PWD/$O/pmc_eager -o run -- python3 $PWD/bench.py $a --no-graph > $O/segv_eager.log 2>&1
+      echo "eager pmc pass rc=$?"
+      MZ_SEGV_MAPS=$PWD/$O/segv_graph.txt timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+        -d $PWD/$O/pmc_graph -o run -- python3 $PWD/bench.py $a > $O/segv_graph.log 2>&1
+      echo "graph pmc pass rc=$?"
+      head -5 $O/segv_graph.txt 2>/dev/null
+      exit 0 ;;
     bench)
       timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?; cat $O/bench.json; [ $rc -ne 0 ] && exit $rc ;;
   esac
