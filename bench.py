@@ -294,7 +294,6 @@ class HipLeg:
             p_move = st["mm_moved"] / backups
             r["normaliser_moved_per_backup"] = round(p_move, 4)
             r["launches_without_a_moved_tree"] = float(f"{(1.0 - p_move) ** B:.3e}")
-        return r
         if span is not None:
             r["launch_span"] = span
         if os.environ.get("MZ_STAMPS") == "1" and st.get("stamped", 0) > 0:
