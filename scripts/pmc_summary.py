@@ -51,7 +51,8 @@ def main():
         kernels[short] = dict(fetch_kb=fetch.get(k), write_kb=write.get(k), dispatches=max(nf.get(k, 0), nw.get(k, 0)))
     def is_fused(k):  # the per-simulation fused kernel: k_chain3 / k_chain / k_tree with selection, or k_step<true,true>
         return ((k.startswith("k_chain<") or k.startswith("k_tree<")) and k.endswith(",true>")) or \
-            (k.startswith("k_chain3<") and ",true," in k) or k.startswith("k_step<true,true")
+            (k.startswith("k_chain3<") and ",true," in k) or k.startswith("k_step<true,true") or \
+            k.startswith("k_hbm<true,true")
     fused = next((v for k, v in kernels.items() if is_fused(k)), {})
     out = {}
     if os.path.exists(args.out):

@@ -21,8 +21,9 @@ declare -A ARGS=(
   [3s5z_k5]="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5"
   [27m_k1]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1"
   [27m_k5]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5"
+  [27m_k16]="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 16"
 )
-CONFIGS=${CONFIGS:-"3m_k1 3m_k5 3m_k10 2s3z_k1 3s5z_k5 3s5z_k10 27m_k1 27m_k5"}
+CONFIGS=${CONFIGS:-"3m_k1 3m_k5 3m_k10 2s3z_k1 3s5z_k5 3s5z_k10 27m_k1 27m_k5 27m_k16"}
 # the PMC passes run first, so the bench lines carry this build's traffic (bench.py reads
 # profiles/pmc_latest.json; on the box that copy is refreshed after every configuration)
 cp profiles/pmc_latest.json gpurun_out/pmc_latest.json 2>/dev/null
@@ -43,8 +44,9 @@ for c in $CONFIGS; do
     # (27m: 27 agent searches x 200 sims = 5,400 fused dispatches per env step; rocprofv3's PMC
     # collection crashed on the host at --steps 3, so those passes profile one step)
     # (27m K = 1 under --pmc with the env step captured as one graph of 5,481 kernel nodes: rocprofv3
-    # segfaults a few seconds into the replay, profiles/round4/pmc_crash_27m_k1_graph.log; the 27m PMC
-    # passes launch eagerly, --no-graph, the same kernels)
+    # segfaults a few seconds into the replay, inside librocprofiler-sdk on an HSA runtime thread,
+    # profiles/round5/pmc_crash_27m_k1_graph_analysis.txt; the 27m PMC passes launch eagerly,
+    # --no-graph, the same kernels)
     ps="--steps 3 --warmup 1"; case $c in 27m*) ps="--steps 1 --warmup 1 --no-graph";; esac
     step "$d/pmc_fetch.json" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$R/$d/pmc_fetch" -o run -- \
         python3 "$R/bench.py" --no-cpu $ps $a

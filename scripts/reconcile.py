@@ -37,7 +37,7 @@ def fused_stats(trace_dir):
         for r in csv.DictReader(open(f)):
             nm = r["Name"]
             if (("k_chain<" in nm or "k_tree<" in nm) and ", true>" in nm) or ("k_chain3<" in nm and ", true," in nm) \
-                    or "k_step<true, true" in nm:
+                    or "k_step<true, true" in nm or "k_hbm<true, true" in nm:
                 return dict(calls=int(r["Calls"]), mean_ns=float(r["AverageNs"]), min_ns=float(r["MinNs"]),
                             max_ns=float(r["MaxNs"]), total_ns=float(r["TotalDurationNs"]))
     return None

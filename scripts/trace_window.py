@@ -83,7 +83,7 @@ def main():
     res = summarise(window(load_trace(a.trace_dir)), steps)
     if b:
         fused = next((k for k in res["kernels"] if (("k_chain<" in k or "k_tree<" in k) and ", true>" in k)
-                      or ("k_chain3<" in k and ", true," in k)), None)
+                      or ("k_chain3<" in k and ", true," in k) or "k_hbm<true, true" in k), None)
         rb = b["roofline"]
         res["bench"] = dict(ms_per_step=b["ms_per_step"], value=b["value"], event_launch_us=rb["avg_launch_us"],
                             bytes_per_launch=rb["bytes_per_launch"], frac=rb["frac"])
