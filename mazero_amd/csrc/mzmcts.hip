@@ -2874,10 +2874,16 @@ __device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp)
     if (A <= 16) return cdf_terms<16>(A, sw, sp, wl);
     return cdf_long(A, sw, sp, wl);
 }
-// the same for the weights bet held one per lane (lane a < A)
-__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp) {
+// the same for the weights bet held one per lane (lane a < A); `during` runs while the weights'
+// LDS store is in flight (independent per-lane work of the caller)
+struct NoWork {
+    __device__ void operator()() const {}
+};
+template <class F = NoWork>
+__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp, F &&during = F()) {
     const int l = lane_id();
     sw[l] = (l < A) ? bet : 0.f;  // kMaxActions = kWave entries
+    during();
     wait_lds();
     if (A <= 4) return cdf_terms<4>(A, sw, sp, bet);
     if (A <= 8) return cdf_terms<8>(A, sw, sp, bet);
@@ -3541,6 +3547,10 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         if (l == 0) {
             sX[0] = mn;
             sX[1] = mx;
+            // (the header's normaliser is this wave's: wave 0 skips the barrier in select_walk's
+            // fast case and writes the rest of the header)
+            hp->mm_min = mn;
+            hp->mm_max = mx;
             if (MZ_STAMPS) {
                 sXl[0] = (long long)(ts[2] - ts[1]);                         // the recurrence
                 sXl[1] = (long long)(__builtin_amdgcn_s_memtime() - ts[2]);  // node updates
@@ -3727,22 +3737,28 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
     const int leaf = D, c = D + 1;  // the new child
     int cursor = h.cursor;
     int a = 0;
+    const float bh = 1.0f;  // betahat_prob = count / sampled_times = 1 / 1
+    // every lane's prior * betahat_prob / beta_prob (eps = 0 after the root), computed while the
+    // distribution's first LDS store is in flight; the drawn lane's is read after the draw
+    float prior_l = 0.f;
     if (A >= 2) {
-        const double cp = cdf_bcast(bet, A, (float *)(smem + L.oW), (double *)(smem + L.oP));
+        const double cp = cdf_bcast(bet, A, (float *)(smem + L.oW), (double *)(smem + L.oP),
+                                    [&]() { prior_l = pol * bh / bet; });
         const double w1 = (double)h.nxt[0], w2 = (double)h.nxt[1];
         double u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
         if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
         a = __popcll(ballot(l < A && cp < u));    // lower_bound
         cursor += 2;
+    } else {
+        prior_l = pol * bh / bet;
     }
     a = uni(a);
     stamp(ts, 2);
     const float omr = i2f(omri);
     if (c + 1 > P) err |= kErrPool;
     if (value_lim(1, omr) != 1) err |= kErrValueSet;  // (count 1: size_lim must be 1, utils.cpp:31)
-    const float bh = 1.0f;  // betahat_prob = count / sampled_times = 1 / 1
     const float pol_a = rlf(pol, a), bet_a = rlf(bet, a);
-    const float prior = pol_a * bh / bet_a;  // prior * betahat_prob / beta_prob (eps = 0 after the root)
+    const float prior = rlf(prior_l, a);
     const bool wild = !tame_prior(prior);
     leaf_b = uni4(leaf_b);
     if (!err && l == 0) {
@@ -3771,9 +3787,13 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         act[t] = err ? 0 : a;
     }
     stamp(ts, 3);
-    lds_barrier();  // wave 1's back-propagation (sA, sPP) and min / max; wave 2's flag
+    // wave 1's back-propagation (sA, sPP) and min / max: read by the exact case and the fused
+    // readback only.  In select_walk's fast case (one word per level) wave 0 takes no barrier (wave
+    // 1's waits for this wave's end instead: s_barrier counts the waves that have not ended)
+    const bool bar = MZ_STAMPS || !SEL || !fast;  // (stamped builds: wave 1's stamps come through LDS)
+    if (bar) lds_barrier();
     stamp(ts, 4);
-    const float mn = unif(sX[0]), mx = unif(sX[1]);
+    const float mn = bar ? unif(sX[0]) : 0.f, mx = bar ? unif(sX[1]) : 0.f;
     const int mm_cnt = D;
     int words = 0;
     if (SEL && fast) {
@@ -3828,9 +3848,7 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
         hp->tot = err ? h.tot : c + 1;
         hp->D = (err || !SEL) ? h.D : Ds;
         hp->err = err;
-        hp->mm_min = mn;
-        hp->mm_max = mx;
-        hp->mm_cnt = mm_cnt;
+        hp->mm_cnt = mm_cnt;  // (mm_min / mm_max: wave 1)
         hp->tame = tame;
         hp->leaf = (err || !SEL) ? h.leaf : c;
     }

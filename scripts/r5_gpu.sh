@@ -19,7 +19,8 @@ for st in $STEPS; do
             3s5z_k5) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5";;
             3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
             27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
-            3m_k1) a="--sampled-times 1";;
+            3m_k1) a="--sampled-times 1";; 2s3z_k1) a="--map 2s3z --roots 1024 --sims 50";;
+            27m_k1) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1";;
           esac
           line="$cfg rep$rep"
           for v in prod ${ALTS:-r4 split}; do
@@ -33,10 +34,20 @@ for st in $STEPS; do
     stamps)
       for cfg in ${STAMPCFG:-3m_k5}; do
         case $cfg in
-          3m_k5) a="--sampled-times 5";; 3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
+          3m_k1) a="--sampled-times 1";; 3m_k5) a="--sampled-times 5";; 3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
           27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
         esac
         MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a > $O/stamps_$cfg.json 2> $O/stamps.err || exit 1
+      done ;;
+    spans)
+      # launch spans (MZ_SPANS build, scripts/build_variant.sh spans -DMZ_SPANS=1): per wave role
+      for cfg in ${STAMPCFG:-3m_k1}; do
+        case $cfg in
+          3m_k1) a="--sampled-times 1";; 3m_k5) a="--sampled-times 5";; 2s3z_k1) a="--map 2s3z --roots 1024 --sims 50";;
+          27m_k1) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1";;
+        esac
+        MZ_LIB_OVERRIDE=$PWD/mazero_amd/_build/variant_spans.so timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a \
+          > $O/spans_$cfg.json 2> $O/spans.err || { tail -5 $O/spans.err; exit 1; }
       done ;;
     segv)
       # the round-3/4 profiler abort: the 27m K = 1 --pmc pass over the env step's graph (5,481 kernel
