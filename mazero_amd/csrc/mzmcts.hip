@@ -2827,11 +2827,14 @@ __device__ __forceinline__ double cdf_terms(int A, const float *sw, double *sp, 
     if (l == A - 1) cp = 1.0;
     return cp;
 }
-// A > 16: batches of 16 terms
+// A > 16: batches of 16 terms, then the rest in steps of 4 up to A rounded up to 4 (27m: 36 terms,
+// not three batches of 16); each batch's LDS reads issued together ahead of its adds
 __device__ __forceinline__ double cdf_long(int A, const float *sw, double *sp, float wl) {
     const int l = lane_id();
+    const int A4 = (A + 3) & ~3;
     double sum = 0.0;
-    for (int a0 = 0; a0 < A; a0 += 16) {
+    int a0 = 0;
+    for (; a0 + 16 <= A4; a0 += 16) {
         float w[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2844,11 +2847,35 @@ __device__ __forceinline__ double cdf_long(int A, const float *sw, double *sp, f
 #pragma unroll
         for (int j = 0; j < 16; ++j) sum += (double)w[j];
     }
+    // 0, 4, 8 or 12 terms left; the three reads are issued together, so with fewer left they run
+    // past sw / sp into the caller's next LDS region (read, never used)
+    const int rest = A4 - a0;
+    if (rest > 0) {
+        const float4 v0 = *(const float4 *)(sw + a0), v1 = *(const float4 *)(sw + a0 + 4),
+                     v2 = *(const float4 *)(sw + a0 + 8);
+        sum += (double)v0.x;
+        sum += (double)v0.y;
+        sum += (double)v0.z;
+        sum += (double)v0.w;
+        if (rest > 4) {
+            sum += (double)v1.x;
+            sum += (double)v1.y;
+            sum += (double)v1.z;
+            sum += (double)v1.w;
+        }
+        if (rest > 8) {
+            sum += (double)v2.x;
+            sum += (double)v2.y;
+            sum += (double)v2.z;
+            sum += (double)v2.w;
+        }
+    }
     const double p = (l < A) ? (double)wl / sum : 0.0;
     sp[l] = p;
     wait_lds();
     double acc = 0.0, cp = 0.0;
-    for (int a0 = 0; a0 < A; a0 += 16) {
+    a0 = 0;
+    for (; a0 + 16 <= A4; a0 += 16) {
         double pj[16];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -2860,6 +2887,34 @@ __device__ __forceinline__ double cdf_long(int A, const float *sw, double *sp, f
         for (int j = 0; j < 16; ++j) {
             acc = (a0 + j == 0) ? pj[0] : acc + pj[j];
             cp = sel_lane(cp, acc, 1ull << (j & 63) << (a0 & 63));
+        }
+    }
+    if (rest > 0) {
+        double pj[12];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
+            pj[2 * q] = v.x;
+            pj[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc = acc + pj[j];
+            cp = sel_lane(cp, acc, 1ull << (a0 + j));
+        }
+        if (rest > 4) {
+#pragma unroll
+            for (int j = 4; j < 8; ++j) {
+                acc = acc + pj[j];
+                cp = sel_lane(cp, acc, 1ull << (a0 + j));
+            }
+        }
+        if (rest > 8) {
+#pragma unroll
+            for (int j = 8; j < 12; ++j) {
+                acc = acc + pj[j];
+                cp = sel_lane(cp, acc, 1ull << (a0 + j));
+            }
         }
     }
     if (l == A - 1) cp = 1.0;
