@@ -700,6 +700,10 @@ __device__ __forceinline__ double sel_lane(double v, double x, unsigned long lon
                                             (unsigned)__float_as_int(lo)));
 }
 
+__device__ __forceinline__ long long sel_lane(long long v, long long x, unsigned long long m) {
+    return __double_as_longlong(sel_lane(__longlong_as_double(v), __longlong_as_double(x), m));
+}
+
 __device__ __forceinline__ double cdf_lane(double bd, int A) {
     const int l = lane_id();
     // Both chains read their operands into SGPRs 8 at a time ahead of the dependent adds (a
@@ -5562,18 +5566,20 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     }
     stamp(ts, 8);
     if (l < kStatN) {
+        // lane l's counter: the uniform values placed by SALU-built lane masks (a switch on the lane
+        // index compiles to a chain of exec-masked branches on this wave's critical path)
         long long add = 0;
-        switch (l) {
-            case MZ_S_SELECTS: add = (err || !SEL) ? 0 : 1; break;
-            case MZ_S_PATH_EDGES: add = Dn; break;
-            case MZ_S_SCORED: add = nscored; break;
-            case MZ_S_EXPANDS: add = 1; break;
-            case MZ_S_NEW_CHILDREN: add = ncl; break;
-            case MZ_S_BACKUP_NODES: add = D + 1; break;
-            case MZ_S_ENTRIES_READ: add = ent_r; break;
-            case MZ_S_ENTRIES_WRITTEN: add = ent_w; break;
-            case MZ_S_MINMAX_NODES: add = tot - 1; break;
-            case MZ_S_MM_MOVED: add = moved; break;
+        add = sel_lane(add, (long long)((err || !SEL) ? 0 : 1), 1ull << MZ_S_SELECTS);
+        add = sel_lane(add, (long long)Dn, 1ull << MZ_S_PATH_EDGES);
+        add = sel_lane(add, nscored, 1ull << MZ_S_SCORED);
+        add = sel_lane(add, 1ll, 1ull << MZ_S_EXPANDS);
+        add = sel_lane(add, (long long)ncl, 1ull << MZ_S_NEW_CHILDREN);
+        add = sel_lane(add, (long long)(D + 1), 1ull << MZ_S_BACKUP_NODES);
+        add = sel_lane(add, ent_r, 1ull << MZ_S_ENTRIES_READ);
+        add = sel_lane(add, ent_w, 1ull << MZ_S_ENTRIES_WRITTEN);
+        add = sel_lane(add, (long long)(tot - 1), 1ull << MZ_S_MINMAX_NODES);
+        add = sel_lane(add, (long long)moved, 1ull << MZ_S_MM_MOVED);
+        if (MZ_STAMPS) switch (l) {
             case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;    // round 1
             case MZ_S_CYC_STAGE2: add = (long long)(ts[2] - ts[1]); break;    // barrier (1) wait
             case MZ_S_CYC_EXPAND: add = (long long)(ts[3] - ts[2]); break;    // draws + children

@@ -44,10 +44,13 @@ for st in $STEPS; do
       for cfg in ${STAMPCFG:-3m_k1}; do
         case $cfg in
           3m_k1) a="--sampled-times 1";; 3m_k5) a="--sampled-times 5";; 2s3z_k1) a="--map 2s3z --roots 1024 --sims 50";;
+          27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
           27m_k1) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1";;
         esac
-        MZ_LIB_OVERRIDE=$PWD/mazero_amd/_build/variant_spans.so timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a \
-          > $O/spans_$cfg.json 2> $O/spans.err || { tail -5 $O/spans.err; exit 1; }
+        for sv in ${SPANV:-spans}; do
+          MZ_LIB_OVERRIDE=$PWD/mazero_amd/_build/variant_$sv.so timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a \
+            > $O/${sv}_$cfg.json 2> $O/spans.err || { tail -5 $O/spans.err; exit 1; }
+        done
       done ;;
     segv)
       # the round-3/4 profiler abort: the 27m K = 1 --pmc pass over the env step's graph (5,481 kernel
