@@ -5104,6 +5104,11 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     h.mm_min = hp0->mm_min;  // (the normaliser before this back-propagation: MZ_S_MM_MOVED)
     h.mm_max = hp0->mm_max;
     h.mm_cnt = hp0->mm_cnt;
+    // (held from here in the level-walk classes: left to the compiler, these were reloaded from the
+    // header by scalar loads where they are used, in the epilogue, each with a wait for its round
+    // trip; same-box A/B, 27m K = 5 11.91 -> 11.78 us.  The other classes' SGPR pressure makes it a
+    // loss there: 3m K = 5 7.54 -> 7.61)
+    if constexpr (kTreeLevels<NC>) asm volatile("" : "+s"(h.tame), "+s"(h.mm_min), "+s"(h.mm_max), "+s"(h.mm_cnt));
     const int gW = pl->g.W;
     const float gdelta = pl->g.delta;
     d.o_D = pl->d.o_D;
