@@ -312,7 +312,7 @@ def launch_spans(spans, S, B):
     buf = (C.c_ulonglong * (4 * slots * trees))()
     spans(C.cast(buf, C.c_void_p), slots, trees, 0)
     raw = np.array(buf[:], dtype=np.uint64).reshape(slots, trees, 4)[1:slots]
-    info = np.where(raw >= np.uint64(1 << 63), raw & np.uint64((1 << 48) - 1), np.uint64(0))  # k_tree: tree shapes
+    info = np.where(raw >= np.uint64(1 << 63), raw & np.uint64((1 << 63) - 1), np.uint64(0))  # k_tree: tree shapes
     t = np.where(raw >= np.uint64(1 << 63), 0, raw).astype(np.float64) * 10.0  # ns
     start = t[:, :, 0]
     ends = np.where(t[:, :, 1:] > 0, t[:, :, 1:], np.nan)
@@ -332,6 +332,20 @@ def launch_spans(spans, S, B):
                                   for k in np.unique(D)},
                      slowest_tree_D=np.bincount(D[np.arange(len(slow)), slow]).tolist(),
                      ntot_max=int(((info[:, :, 2] >> np.uint64(16)) & np.uint64(0xffff)).max()))
+        # the trees after whose back-propagation the min/max normaliser moved (bit 48): every score
+        # of such a tree changes, so an incremental rescore (only the path's parents) helps only the
+        # others.  A launch ends with its slowest tree: the slowest moved tree per launch bounds what
+        # skipping the rescore in every other tree could give
+        mv = ((info[:, :, 2] >> np.uint64(48)) & np.uint64(1)).astype(bool)
+        if mv.any():
+            own_mv = np.where(mv, own, np.nan)
+            own_st = np.where(mv, np.nan, own)
+            shape["normaliser_moved"] = dict(
+                trees_per_launch=round(float(mv.sum(axis=1).mean()), 1),
+                slowest_tree_us=round(float(np.nanmean(np.nanmax(own, axis=1))) / 1e3, 3),
+                slowest_moved_tree_us=round(float(np.nanmean(np.nanmax(own_mv, axis=1))) / 1e3, 3),
+                slowest_unmoved_tree_us=round(float(np.nanmean(np.nanmax(own_st, axis=1))) / 1e3, 3),
+                launches_whose_slowest_tree_moved=round(float(mv[np.arange(len(own)), np.nanargmax(own, axis=1)].mean()), 3))
         ph = info[:, :, 3]
         if ph.any():  # wave 0's phase ends by D: barrier (1) left, barrier (2) left, chase done, end (us)
             marks = [((ph >> np.uint64(16 * k)) & np.uint64(0xffff)).astype(np.float64) * 0.01 for k in range(3)]

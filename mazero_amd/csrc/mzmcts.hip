@@ -5612,7 +5612,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     if (l == 0 && err) atomicOr(d.err(), err);
     span_close(hsx, rt0);
     span_info(hsx, (unsigned long long)(D & 0xffff) | ((unsigned long long)(ntot & 0xffff) << 16) |
-                       ((unsigned long long)(Dn & 0xffff) << 32), rt0, rm1, rm2, rm3);
+                       ((unsigned long long)(Dn & 0xffff) << 32) | ((unsigned long long)moved << 48), rt0, rm1, rm2, rm3);
 }
 
 // mz_create's device initialisation in one launch (instead of three copies and three memsets,

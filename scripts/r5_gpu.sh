@@ -45,6 +45,8 @@ for st in $STEPS; do
         case $cfg in
           3m_k1) a="--sampled-times 1";; 3m_k5) a="--sampled-times 5";; 2s3z_k1) a="--map 2s3z --roots 1024 --sims 50";;
           27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
+          3m_k10) a="--sampled-times 10";; 3s5z_k5) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5";;
+          3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
           27m_k1) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1";;
         esac
         for sv in ${SPANV:-spans}; do
