@@ -21,6 +21,7 @@ for st in $STEPS; do
             27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
             3m_k1) a="--sampled-times 1";; 2s3z_k1) a="--map 2s3z --roots 1024 --sims 50";;
             27m_k1) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 1";;
+            27m_k16) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 16";;
           esac
           line="$cfg rep$rep"
           for v in prod ${ALTS:-r4 split}; do
@@ -36,6 +37,7 @@ for st in $STEPS; do
         case $cfg in
           3m_k1) a="--sampled-times 1";; 3m_k5) a="--sampled-times 5";; 3s5z_k10) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 10";;
           27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
+          27m_k16) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 16";;
         esac
         MZ_STAMPS=1 timeout -k 10 200 python bench.py --no-cpu --steps 3 --warmup 1 $a > $O/stamps_$cfg.json 2> $O/stamps.err || exit 1
       done ;;
