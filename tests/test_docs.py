@@ -3,7 +3,7 @@
 DESIGN.md / README.md / INTEGRATION.md / scripts/README.md quote numbers from `profiles/` and name
 files of this repository.  These checks keep them from drifting: every repository file they name
 exists, README's headline is the committed headline bench line, and DESIGN §5's configuration table
-is the committed reconciliation (`profiles/round4/roofline_reconcile.json`)."""
+is the committed reconciliation (`profiles/round5/roofline_reconcile.json`)."""
 from __future__ import annotations
 
 import json
@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOCS = ["DESIGN.md", "README.md", "INTEGRATION.md", os.path.join("scripts", "README.md")]
-ROUND = os.path.join(ROOT, "profiles", "round4")
+ROUND = os.path.join(ROOT, "profiles", "round5")
 
 # names of the reference's own sources (in /root/reference, cited by file:line) and of files a
 # document says are gone
@@ -41,7 +41,8 @@ def test_named_files_exist(doc):
             assert os.path.exists(os.path.join(ROUND, "3m_k1", n)), n
             continue
         cands = [n] + [os.path.join(d, n) for d in ("scripts", "mazero_amd", "mazero_amd/csrc", "oracle", "include",
-                                                     "tests", "profiles/round4", "profiles/round3", "profiles")]
+                                                     "tests", "profiles/round5", "profiles/round4", "profiles/round3",
+                                                     "profiles")]
         if not any(os.path.exists(os.path.join(ROOT, c)) for c in cands):
             missing.append(n)
     assert not missing, f"{doc} names files that do not exist: {missing}"
@@ -66,7 +67,9 @@ def test_design_table_is_the_committed_reconciliation():
     with open(os.path.join(ROUND, "roofline_reconcile.json")) as f:
         rec = json.load(f)
     rows = {}
-    for line in _read("DESIGN.md").splitlines():
+    text = _read("DESIGN.md")
+    sec = text[text.index("## 5. Measurement (round 5"):text.index("### Round 4 (for the record)")]
+    for line in sec.splitlines():
         m = re.match(r"\| (3m|2s3z|3s5z_vs_3s6z|27m_vs_30m) (\d+)×(\d+) K=(\d+) \| ([0-9.]+) M \| [^|]+\| ([0-9.]+) µs \|",
                      line)
         if m:
