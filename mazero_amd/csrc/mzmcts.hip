@@ -744,6 +744,166 @@ __device__ __forceinline__ double cdf_lane(double bd, int A) {
     return cp;
 }
 
+// std::discrete_distribution's cumulative table (libstdc++ random.tcc:2656-2690, as cdf_lane) for
+// the weights staged in sw[0 .. 64) (sw[l] = 0 for l >= A; lane l's own weight is wl): the
+// sequential double sum and the sequential prefix sums run on every lane from broadcast LDS reads
+// instead of v_readlane.  N terms (A <= N): trailing +0.0 terms are exact no-ops on the
+// non-negative sums, so N only has to cover A -- the class (4, 8, 12, 16) is picked once per call,
+// not per term.  Lane a returns cp[a] (cp[A-1] forced to 1.0).
+template <int N>
+__device__ __forceinline__ double cdf_terms(int A, const float *sw, double *sp, float wl) {
+    const int l = lane_id();
+    float w[N];
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) {
+        const float4 v = *(const float4 *)(sw + 4 * q);
+        w[4 * q] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) sum += (double)w[j];
+    const double p = (l < A) ? (double)wl / sum : 0.0;
+    sp[l] = p;
+    wait_lds();
+    double pj[N];
+#pragma unroll
+    for (int q = 0; q < N / 2; ++q) {
+        const double2 v = *(const double2 *)(sp + 2 * q);
+        pj[2 * q] = v.x;
+        pj[2 * q + 1] = v.y;
+    }
+    double acc = pj[0], cp = (l == 0) ? pj[0] : 0.0;
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        acc = acc + pj[j];
+        cp = sel_lane(cp, acc, 1ull << j);
+    }
+    if (l == A - 1) cp = 1.0;
+    return cp;
+}
+// A > 16: batches of 16 terms, then the rest in steps of 4 up to A rounded up to 4 (27m: 36 terms,
+// not three batches of 16); each batch's LDS reads issued together ahead of its adds
+__device__ __forceinline__ double cdf_long(int A, const float *sw, double *sp, float wl) {
+    const int l = lane_id();
+    const int A4 = (A + 3) & ~3;
+    double sum = 0.0;
+    int a0 = 0;
+    for (; a0 + 16 <= A4; a0 += 16) {
+        float w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float4 v = *(const float4 *)(sw + a0 + 4 * q);
+            w[4 * q] = v.x;
+            w[4 * q + 1] = v.y;
+            w[4 * q + 2] = v.z;
+            w[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += (double)w[j];
+    }
+    // 0, 4, 8 or 12 terms left; the three reads are issued together, so with fewer left they run
+    // past sw / sp into the caller's next LDS region (read, never used)
+    const int rest = A4 - a0;
+    if (rest > 0) {
+        const float4 v0 = *(const float4 *)(sw + a0), v1 = *(const float4 *)(sw + a0 + 4),
+                     v2 = *(const float4 *)(sw + a0 + 8);
+        sum += (double)v0.x;
+        sum += (double)v0.y;
+        sum += (double)v0.z;
+        sum += (double)v0.w;
+        if (rest > 4) {
+            sum += (double)v1.x;
+            sum += (double)v1.y;
+            sum += (double)v1.z;
+            sum += (double)v1.w;
+        }
+        if (rest > 8) {
+            sum += (double)v2.x;
+            sum += (double)v2.y;
+            sum += (double)v2.z;
+            sum += (double)v2.w;
+        }
+    }
+    const double p = (l < A) ? (double)wl / sum : 0.0;
+    sp[l] = p;
+    wait_lds();
+    double acc = 0.0, cp = 0.0;
+    a0 = 0;
+    for (; a0 + 16 <= A4; a0 += 16) {
+        double pj[16];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
+            pj[2 * q] = v.x;
+            pj[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            acc = (a0 + j == 0) ? pj[0] : acc + pj[j];
+            cp = sel_lane(cp, acc, 1ull << (j & 63) << (a0 & 63));
+        }
+    }
+    if (rest > 0) {
+        double pj[12];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
+            pj[2 * q] = v.x;
+            pj[2 * q + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc = acc + pj[j];
+            cp = sel_lane(cp, acc, 1ull << (a0 + j));
+        }
+        if (rest > 4) {
+#pragma unroll
+            for (int j = 4; j < 8; ++j) {
+                acc = acc + pj[j];
+                cp = sel_lane(cp, acc, 1ull << (a0 + j));
+            }
+        }
+        if (rest > 8) {
+#pragma unroll
+            for (int j = 8; j < 12; ++j) {
+                acc = acc + pj[j];
+                cp = sel_lane(cp, acc, 1ull << (a0 + j));
+            }
+        }
+    }
+    if (l == A - 1) cp = 1.0;
+    return cp;
+}
+// cdf for weights already staged in sw[0..A) (sw[l] = 0 for l >= A)
+__device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp) {
+    const float wl = sw[lane_id()];
+    if (A <= 4) return cdf_terms<4>(A, sw, sp, wl);
+    if (A <= 8) return cdf_terms<8>(A, sw, sp, wl);
+    if (A <= 12) return cdf_terms<12>(A, sw, sp, wl);
+    if (A <= 16) return cdf_terms<16>(A, sw, sp, wl);
+    return cdf_long(A, sw, sp, wl);
+}
+// the same for the weights bet held one per lane (lane a < A); `during` runs while the weights'
+// LDS store is in flight (independent per-lane work of the caller)
+struct NoWork {
+    __device__ void operator()() const {}
+};
+template <class F = NoWork>
+__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp, F &&during = F()) {
+    const int l = lane_id();
+    sw[l] = (l < A) ? bet : 0.f;  // kMaxActions = kWave entries
+    during();
+    wait_lds();
+    if (A <= 4) return cdf_terms<4>(A, sw, sp, bet);
+    if (A <= 8) return cdf_terms<8>(A, sw, sp, bet);
+    if (A <= 12) return cdf_terms<12>(A, sw, sp, bet);
+    if (A <= 16) return cdf_terms<16>(A, sw, sp, bet);
+    return cdf_long(A, sw, sp, bet);
+}
+
 // --------------------------------------------------------------------------------------------
 // CTree::expand (cnode.cpp:224-295) for one node, agent_num = 1.  Lane a < A holds the node's
 // policy / beta / noise entry for action a.  Children are created for the distinct sampled actions
@@ -757,7 +917,7 @@ __device__ __forceinline__ double cdf_lane(double bd, int A) {
 __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, int parent, float pol, float bet, float noi, float eps,
                            int K, float pv, int &cursor, int &tot, const unsigned *win, int wbase, Lds *s, int &err,
                            long long &st_new, bool have_w, unsigned w1r, unsigned w2r, long long *stl, int &wild,
-                           int *first_act = nullptr) {
+                           int *first_act = nullptr, float *cdf_w = nullptr, double *cdf_p = nullptr) {
     const int l = lane_id();
     const int A = g.A;
     int cnt = 0;  // number of draws that hit action l
@@ -766,7 +926,8 @@ __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, in
     if (A < 2) {
         cnt = (l == 0) ? K : 0;
     } else {
-        const double cp = cdf_lane((l < A) ? (double)bet : 0.0, A);
+        // (with LDS scratch of 64 floats + 64 doubles: the same chains from LDS broadcasts, cdf_bcast)
+        const double cp = cdf_w ? cdf_bcast((l < A) ? bet : 0.f, A, cdf_w, cdf_p) : cdf_lane((l < A) ? (double)bet : 0.0, A);
         if (MZ_STAMPS && stl) {
             asm volatile("" ::"v"(cp));
             e1 = __builtin_amdgcn_s_memtime();
@@ -2789,166 +2950,6 @@ typedef float f32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ldsc4(const float4 *p) {  // (one s_load_dwordx4)
     const f32x4v v = *(const __attribute__((address_space(4))) f32x4v *)p;
     return make_float4(v.x, v.y, v.z, v.w);
-}
-
-// std::discrete_distribution's cumulative table (libstdc++ random.tcc:2656-2690, as cdf_lane) for
-// the weights staged in sw[0 .. 64) (sw[l] = 0 for l >= A; lane l's own weight is wl): the
-// sequential double sum and the sequential prefix sums run on every lane from broadcast LDS reads
-// instead of v_readlane.  N terms (A <= N): trailing +0.0 terms are exact no-ops on the
-// non-negative sums, so N only has to cover A -- the class (4, 8, 12, 16) is picked once per call,
-// not per term.  Lane a returns cp[a] (cp[A-1] forced to 1.0).
-template <int N>
-__device__ __forceinline__ double cdf_terms(int A, const float *sw, double *sp, float wl) {
-    const int l = lane_id();
-    float w[N];
-#pragma unroll
-    for (int q = 0; q < N / 4; ++q) {
-        const float4 v = *(const float4 *)(sw + 4 * q);
-        w[4 * q] = v.x;
-        w[4 * q + 1] = v.y;
-        w[4 * q + 2] = v.z;
-        w[4 * q + 3] = v.w;
-    }
-    double sum = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) sum += (double)w[j];
-    const double p = (l < A) ? (double)wl / sum : 0.0;
-    sp[l] = p;
-    wait_lds();
-    double pj[N];
-#pragma unroll
-    for (int q = 0; q < N / 2; ++q) {
-        const double2 v = *(const double2 *)(sp + 2 * q);
-        pj[2 * q] = v.x;
-        pj[2 * q + 1] = v.y;
-    }
-    double acc = pj[0], cp = (l == 0) ? pj[0] : 0.0;
-#pragma unroll
-    for (int j = 1; j < N; ++j) {
-        acc = acc + pj[j];
-        cp = sel_lane(cp, acc, 1ull << j);
-    }
-    if (l == A - 1) cp = 1.0;
-    return cp;
-}
-// A > 16: batches of 16 terms, then the rest in steps of 4 up to A rounded up to 4 (27m: 36 terms,
-// not three batches of 16); each batch's LDS reads issued together ahead of its adds
-__device__ __forceinline__ double cdf_long(int A, const float *sw, double *sp, float wl) {
-    const int l = lane_id();
-    const int A4 = (A + 3) & ~3;
-    double sum = 0.0;
-    int a0 = 0;
-    for (; a0 + 16 <= A4; a0 += 16) {
-        float w[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float4 v = *(const float4 *)(sw + a0 + 4 * q);
-            w[4 * q] = v.x;
-            w[4 * q + 1] = v.y;
-            w[4 * q + 2] = v.z;
-            w[4 * q + 3] = v.w;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sum += (double)w[j];
-    }
-    // 0, 4, 8 or 12 terms left; the three reads are issued together, so with fewer left they run
-    // past sw / sp into the caller's next LDS region (read, never used)
-    const int rest = A4 - a0;
-    if (rest > 0) {
-        const float4 v0 = *(const float4 *)(sw + a0), v1 = *(const float4 *)(sw + a0 + 4),
-                     v2 = *(const float4 *)(sw + a0 + 8);
-        sum += (double)v0.x;
-        sum += (double)v0.y;
-        sum += (double)v0.z;
-        sum += (double)v0.w;
-        if (rest > 4) {
-            sum += (double)v1.x;
-            sum += (double)v1.y;
-            sum += (double)v1.z;
-            sum += (double)v1.w;
-        }
-        if (rest > 8) {
-            sum += (double)v2.x;
-            sum += (double)v2.y;
-            sum += (double)v2.z;
-            sum += (double)v2.w;
-        }
-    }
-    const double p = (l < A) ? (double)wl / sum : 0.0;
-    sp[l] = p;
-    wait_lds();
-    double acc = 0.0, cp = 0.0;
-    a0 = 0;
-    for (; a0 + 16 <= A4; a0 += 16) {
-        double pj[16];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
-            pj[2 * q] = v.x;
-            pj[2 * q + 1] = v.y;
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            acc = (a0 + j == 0) ? pj[0] : acc + pj[j];
-            cp = sel_lane(cp, acc, 1ull << (j & 63) << (a0 & 63));
-        }
-    }
-    if (rest > 0) {
-        double pj[12];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            const double2 v = *(const double2 *)(sp + a0 + 2 * q);
-            pj[2 * q] = v.x;
-            pj[2 * q + 1] = v.y;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            acc = acc + pj[j];
-            cp = sel_lane(cp, acc, 1ull << (a0 + j));
-        }
-        if (rest > 4) {
-#pragma unroll
-            for (int j = 4; j < 8; ++j) {
-                acc = acc + pj[j];
-                cp = sel_lane(cp, acc, 1ull << (a0 + j));
-            }
-        }
-        if (rest > 8) {
-#pragma unroll
-            for (int j = 8; j < 12; ++j) {
-                acc = acc + pj[j];
-                cp = sel_lane(cp, acc, 1ull << (a0 + j));
-            }
-        }
-    }
-    if (l == A - 1) cp = 1.0;
-    return cp;
-}
-// cdf for weights already staged in sw[0..A) (sw[l] = 0 for l >= A)
-__device__ __forceinline__ double cdf_staged(int A, const float *sw, double *sp) {
-    const float wl = sw[lane_id()];
-    if (A <= 4) return cdf_terms<4>(A, sw, sp, wl);
-    if (A <= 8) return cdf_terms<8>(A, sw, sp, wl);
-    if (A <= 12) return cdf_terms<12>(A, sw, sp, wl);
-    if (A <= 16) return cdf_terms<16>(A, sw, sp, wl);
-    return cdf_long(A, sw, sp, wl);
-}
-// the same for the weights bet held one per lane (lane a < A); `during` runs while the weights'
-// LDS store is in flight (independent per-lane work of the caller)
-struct NoWork {
-    __device__ void operator()() const {}
-};
-template <class F = NoWork>
-__device__ __forceinline__ double cdf_bcast(float bet, int A, float *sw, double *sp, F &&during = F()) {
-    const int l = lane_id();
-    sw[l] = (l < A) ? bet : 0.f;  // kMaxActions = kWave entries
-    during();
-    wait_lds();
-    if (A <= 4) return cdf_terms<4>(A, sw, sp, bet);
-    if (A <= 8) return cdf_terms<8>(A, sw, sp, bet);
-    if (A <= 12) return cdf_terms<12>(A, sw, sp, bet);
-    if (A <= 16) return cdf_terms<16>(A, sw, sp, bet);
-    return cdf_long(A, sw, sp, bet);
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
