@@ -945,7 +945,14 @@ __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, in
                 u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
                 if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
             }
-            for (int k = 0; k < nk; ++k) {
+            int k = 0;
+            for (; k + 4 <= nk; k += 4) {  // (four draws per step, as k_tree)
+                const double u0 = rld(u, k), u1 = rld(u, k + 1), u2 = rld(u, k + 2), u3 = rld(u, k + 3);
+                const int i0 = __popcll(ballot(l < A && cp < u0)), i1 = __popcll(ballot(l < A && cp < u1));
+                const int i2 = __popcll(ballot(l < A && cp < u2)), i3 = __popcll(ballot(l < A && cp < u3));
+                cnt += ((i0 == l) ? 1 : 0) + ((i1 == l) ? 1 : 0) + ((i2 == l) ? 1 : 0) + ((i3 == l) ? 1 : 0);
+            }
+            for (; k < nk; ++k) {
                 const double uk = rld(u, k);
                 const int idx = __popcll(ballot(l < A && cp < uk));
                 cnt += (l == idx) ? 1 : 0;
@@ -5211,7 +5218,16 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         if (cursor + 2 * K > gW || 2 * K > kRngWin) err |= kErrRng;
         // draw k's lower_bound (the actions whose cumulative probability is below u_k) as one ballot
         // over the CDF, one action per lane; lane a counts the draws that chose action a
-        for (int k = 0; k < K; ++k) {
+        // (four draws per step: their readlanes and ballots issue back to back; the compiler does
+        // not unroll a runtime-count loop over convergent operations by itself)
+        int k = 0;
+        for (; k + 4 <= K; k += 4) {
+            const double u0 = rld(u, k), u1 = rld(u, k + 1), u2 = rld(u, k + 2), u3 = rld(u, k + 3);
+            const int i0 = __popcll(ballot(l < A && cp < u0)), i1 = __popcll(ballot(l < A && cp < u1));
+            const int i2 = __popcll(ballot(l < A && cp < u2)), i3 = __popcll(ballot(l < A && cp < u3));
+            cnt += ((i0 == l) ? 1 : 0) + ((i1 == l) ? 1 : 0) + ((i2 == l) ? 1 : 0) + ((i3 == l) ? 1 : 0);
+        }
+        for (; k < K; ++k) {
             const double uk = rld(u, k);
             const int ix = __popcll(ballot(l < A && cp < uk));
             cnt += (ix == l) ? 1 : 0;
