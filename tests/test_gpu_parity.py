@@ -270,6 +270,29 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
 
 
+@pytest.mark.parametrize("K,S", [(3, 700), (2, 40)], ids=["k3_s700", "k2_s40"])
+def test_hbm_wave_per_node_backup(gpu_lib, port_lib, K, S, monkeypatch):
+    """k_hbm's back-propagation (hbm_node_wave, round 5): one wave per path node, dealt over three
+    waves.  S = 700 puts more than 512 entries in the root's value set (the batched two-pass count
+    and tail move instead of the registers); S = 40 keeps every node in registers.  Forced with
+    MZ_HBM=1, against the port."""
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    B, A = 8, 9
+    rng = np.random.default_rng(4242 + S)
+    inp = make_search_inputs(rng, B, A, S)
+    knobs = {}
+    exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
+    monkeypatch.setenv("MZ_HBM", "1")
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    monkeypatch.delenv("MZ_HBM")
+    assert tb.fused_kernel() == "k_hbm"
+    out, _ = run_fused(tb, to_device(inp), K, knobs)
+    exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, exp, f"gpu k_hbm K={K} S={S} ")
+    assert (out["sampled_visit_count"].sum(axis=1) == S).all()
+
+
 @pytest.mark.parametrize("seeding", ["table", "chain", "beyond_table"])
 @pytest.mark.parametrize("K", [1, 5])
 def test_seeding_paths_vs_port(gpu_lib, port_lib, seeding, K, monkeypatch):
