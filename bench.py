@@ -369,7 +369,7 @@ def fused_kernel_name(tb) -> str:
     k = tb.fused_kernel()
     what = {"k_chain3": "K = 1 chains, three waves", "k_chain": "K = 1 chains, two waves",
             "k_tree": "eight waves", "k_step": "general kernel",
-            "k_hbm": "HBM-resident general kernel, four waves"}[k.split("<")[0]]
+            "k_hbm": "HBM-resident general kernel, eight waves"}[k.split("<")[0]]
     return f"{k} ({what}: fused expand+backup+select+gather)"
 
 

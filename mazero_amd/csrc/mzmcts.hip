@@ -945,6 +945,31 @@ __device__ __forceinline__ int expand_node(const Geo &g, const Dev &d, int t, in
                 u = (w1 + w2 * 4294967296.0) / 18446744073709551616.0;
                 if (u >= 1.0) u = 0x1.fffffffffffffp-1;  // nextafter(1, 0)
             }
+            if (cdf_w) {
+                // with LDS scratch: lane k takes draw k0 + k and counts the actions whose cp is below its
+                // u from the broadcast CDF (lanes >= A hold +inf: never below), the same count as the
+                // ballot's popcount; the draws' counts per action by LDS atomics
+                int *hits = (int *)cdf_w;
+                if (k0 == 0) {
+                    cdf_p[l] = (l < A) ? cp : INFINITY;
+                    hits[l] = 0;
+                    wait_lds();
+                }
+                if (l < nk) {
+                    int ix = 0;
+                    const int A4 = (A + 3) & ~3;
+                    for (int a0 = 0; a0 < A4; a0 += 4) {
+                        const double2 c01 = *(const double2 *)(cdf_p + a0), c23 = *(const double2 *)(cdf_p + a0 + 2);
+                        ix += (c01.x < u ? 1 : 0) + (c01.y < u ? 1 : 0) + (c23.x < u ? 1 : 0) + (c23.y < u ? 1 : 0);
+                    }
+                    atomicAdd(&hits[ix], 1);
+                }
+                if (k0 + kWave >= K) {
+                    wait_lds();
+                    cnt = (l < A) ? hits[l] : 0;
+                }
+                continue;
+            }
             int k = 0;
             for (; k + 4 <= nk; k += 4) {  // (four draws per step, as k_tree)
                 const double u0 = rld(u, k), u1 = rld(u, k + 1), u2 = rld(u, k + 2), u3 = rld(u, k + 3);
