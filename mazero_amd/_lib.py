@@ -41,3 +41,18 @@ def load() -> C.CDLL:
             raise RuntimeError(f"{path} is not the hip-gfx950 backend of ABI 1")
         _lib = lib
         return lib
+
+
+def trim_caches() -> int:
+    """Free the device arenas and pinned stages that destroyed handles left in the library's
+    process-wide caches (mz_trim_caches, include/mzdriver.h); returns the bytes released.  A
+    process that has not loaded the library has nothing cached: 0, without loading it."""
+    with _lock:
+        lib = _lib
+    if lib is None:
+        return 0
+    n = C.c_int64(0)
+    rc = lib.mz_trim_caches(C.byref(n))
+    if rc != 0:
+        raise RuntimeError(f"mz_trim_caches: {lib.mz_last_error().decode(errors='replace')}")
+    return int(n.value)

@@ -332,14 +332,18 @@ def _evict_loops_of(tb) -> None:
         del _LOOPS[k]
 
 
-def release() -> None:
+def release() -> int:
     """Drop every cached tree handle, search loop (its graph) and hidden-state pool, of every thread
-    (what the reference frees after each search, mcts_sampled.py:86,89).  The next search of a
-    geometry allocates and records again."""
+    (what the reference frees after each search, mcts_sampled.py:86,89), then free the device arenas
+    the destroyed handles returned to the library's cache (mz_trim_caches).  The next search of a
+    geometry allocates and records again.  Returns the bytes the library released."""
     with _LOCK:
         _LOOPS.clear()
         _TREES.clear()
         _POOLS.clear()
+    from ._lib import trim_caches
+
+    return trim_caches()
 
 
 def half_exp_table() -> np.ndarray:

@@ -780,6 +780,10 @@ def test_agent_loops_share_one_pool(port_lib):
     ms.release()
     gc.collect()
     assert all(r() is None for r in pools)  # release() freed every pool
+    ms.release()  # (the handles' arenas, returned to the library's cache when they died: freed)
+    from mazero_amd._lib import trim_caches
+
+    assert trim_caches() == 0
 
 
 # ------------------------------------------------------------------------------------------------

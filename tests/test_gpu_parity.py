@@ -270,6 +270,25 @@ def test_baseline_sizes_vs_port(gpu_lib, port_lib, name, B, A, K, S, lz):
     assert np.allclose(bh, 1.0, atol=1e-5)  # beta_hat = counts / K over the K root draws
 
 
+def test_trim_caches_releases_destroyed_arenas(gpu_lib):
+    """A destroyed handle's device arena goes to the library's process-wide cache (reused by the next
+    handle of a fitting size); mz_trim_caches (mazero_amd._lib.trim_caches, called by
+    mcts_sampled.release) frees what the cache holds."""
+    import gc
+
+    from mazero_amd._lib import trim_caches
+    from mazero_amd.synthetic import make_search_inputs
+
+    trim_caches()
+    inp = make_search_inputs(np.random.default_rng(7), 64, 9, 20)
+    tb = make_tb(gpu_lib, inp, 5, {})
+    torch.cuda.synchronize()
+    del tb
+    gc.collect()
+    assert trim_caches() > 0
+    assert trim_caches() == 0
+
+
 @pytest.mark.parametrize("K,S", [(3, 700), (2, 40)], ids=["k3_s700", "k2_s40"])
 def test_hbm_wave_per_node_backup(gpu_lib, port_lib, K, S, monkeypatch):
     """k_hbm's back-propagation (hbm_node_wave, round 5): one wave per path node, dealt over three
