@@ -5067,9 +5067,31 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             tree_select_prep<NC>(smem, 1, e ? tot : tot + ncl, discount, gdel, PS, D);
             if (w1g && pool && !e) {
                 // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[parent's hsx][t], after
-                // this wave's copy of wave 0's chase (no path record)
+                // this wave's copy of wave 0's chase; while the row's loads are in flight, the path
+                // record {node, visits at selection} for the next back-propagation and the scored
+                // children's count (wave 0's epilogue leaves both to this wave)
                 int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0;
-                tree_chase<NC, false>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px);
+                tree_chase<NC, true>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px);
+                auto write_path = [&]() {
+                    int2 *gp = d.path() + (size_t)t * PS;
+                    const int2 *sPath1 = (const int2 *)(smem + L::oPath);
+                    const int *sFl1 = (const int *)(smem + L::oFl);
+                    const int4 *sA1 = (const int4 *)(smem + L::oA);
+                    int nsc = 0;
+                    for (int i0 = 0; i0 <= Dn; i0 += kWave) {
+                        const int i = i0 + l;
+                        if (i <= Dn) {
+                            const int xi_ = (i < kWave) ? px : sPath1[i].x;
+                            const int vis = sA1[xi_].x + (sFl1[xi_] ? 1 : 0);
+                            gp[i] = make_int2(xi_, vis);
+                            const int nci = nc_of(sB[xi_].y);
+                            if (i < Dn && !(i == 0 && vis <= nci)) nsc += nci;  // scored levels
+                        }
+                    }
+                    const long long nscored = wave_sum(nsc);
+                    const long long *sSt1 = (const long long *)(smem + L::oSt);
+                    if (l == 0) d.stats()[(size_t)t * MZ_S_COUNT + MZ_S_SCORED] = sSt1[MZ_S_SCORED] + nscored;
+                };
                 if (!e) {
                     const int oi = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
                     const char *src = pool + (long long)oi * pool_stride + (long long)t * row_bytes;
@@ -5084,15 +5106,18 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                         const int4 v1 = *(const int4 *)(src + (o + 1024 < last ? o + 1024 : last));
                         const int4 v2 = *(const int4 *)(src + (o + 2048 < last ? o + 2048 : last));
                         const int4 v3 = *(const int4 *)(src + (o + 3072 < last ? o + 3072 : last));
+                        write_path();
                         if (o < row_bytes) *(int4 *)(gdst + o) = v0;
                         if (o + 1024 < row_bytes) *(int4 *)(gdst + o + 1024) = v1;
                         if (o + 2048 < row_bytes) *(int4 *)(gdst + o + 2048) = v2;
                         if (o + 3072 < row_bytes) *(int4 *)(gdst + o + 3072) = v3;
                     } else if (al) {
                         for (long long o2 = o; o2 < row_bytes; o2 += 16 * kWave) *(int4 *)(gdst + o2) = *(const int4 *)(src + o2);
+                        write_path();
                     } else {
                         for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
                             *(int *)(gdst + o2) = *(const int *)(src + o2);
+                        write_path();
                     }
                 }
             }
@@ -5521,7 +5546,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #ifdef MZ_SPANS_EPI
     rm1 = span_mark();
 #endif
-    if (SEL && !err) {
+    const bool w1path = SEL && w1g && pool;  // (wave 1 writes the path record and the scored count)
+    if (SEL && !err && !w1path) {
         // the path {node, visits at selection} for the next back-propagation (and the scored
         // children), while the row's loads are in flight
         wait_lds();
@@ -5649,7 +5675,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             case MZ_S_CYC_BAK_WAIT: add = MZ_STAMPS ? xl[9] : 0; break;       // wave 3: all after (1)
             default: break;
         }
-        st[l] = st_old + add;
+        if (!(w1path && l == MZ_S_SCORED)) st[l] = st_old + add;
     }
     if (l == 0 && err) atomicOr(d.err(), err);
     span_close(hsx, rt0);
