@@ -4983,6 +4983,43 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         if (SEL && !kTreeLevels<NC> && wv < 4) {
             const int ncl = uni(xi[15]), err = bk_err<NC>(smem) | uni(xi[14]);
             tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, gdel, PS, D);
+            if (wv == 2 && w1g && pool && !err) {
+                // where wave 1 gathers the row and writes the path record, this wave runs a third
+                // copy of the chase and writes the header but its tame flag (wave 0's), so that wave
+                // 0's epilogue is the selection outputs and the counters
+                const int gW2 = pl->g.W;
+                d.o_R = pl->d.o_R;
+                int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0, e = 0;
+                tree_chase<NC, false>(smem, d, t, gW2, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px);
+                if (!e) {
+                    TreeHdr *hp = d.hdr() + t;
+                    const int wb = uni(xi[62]), ws = uni(xi[59]);
+                    const int o0 = cur - wb + ws;
+                    const unsigned *sRng2 = (const unsigned *)(smem + L::oRng);
+                    if (uni((int)(o0 >= ws && o0 + kNxt <= kRngWin))) {
+                        if (l < kNxt) hp->nxt[l] = sRng2[o0 + l];
+                    } else {  // beyond the window (rare)
+                        unsigned *scr = (unsigned *)(smem + L::oIx);
+                        const int w = cur + l < gW2 ? cur + l : gW2 - 1;
+                        glds4a(d.R() + (size_t)t * gW2 + w, scr);
+                        wait_vm();
+                        if (l < kNxt) hp->nxt[l] = (cur + l < gW2) ? scr[l] : 0u;
+                    }
+                    float mn2, mx2;
+                    int cnt2;
+                    bk_minmax<NC>(smem, D, mn2, mx2, cnt2);
+                    if (l == 0) {
+                        hp->cursor = cur;
+                        hp->tot = tot + ncl;
+                        hp->D = Dn;
+                        hp->err = 0;
+                        hp->mm_min = mn2;
+                        hp->mm_max = mx2;
+                        hp->mm_cnt = cnt2;
+                        hp->leaf = x;
+                    }
+                }
+            }
         }
         wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
@@ -4994,6 +5031,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         bk_path_records<BK>(d, t, PS, 0, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
         const int gW1 = pl->g.W;
+        d.o_R = pl->d.o_R;  // (its copy of the chase reads words past the LDS window from the stream)
         if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
         dma_dwords(d.lp(), lds_addr(smem) + L::oLp, PS + 1, true);
         unsigned long long tw1[4] = {0};
@@ -5573,7 +5611,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #ifdef MZ_SPANS_EPI
     rm2 = span_mark();
 #endif
-    {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
+    if (w1path && !err) {  // (wave 2 writes the rest of the header)
+        if (l == 0) d.hdr()[t].tame = h.tame;
+    } else {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
         const int cur = err ? h.cursor : cursor;
         const int o0 = cur - wbase + wsh;
         TreeHdr *hp = d.hdr() + t;
