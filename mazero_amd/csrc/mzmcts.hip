@@ -4792,6 +4792,14 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     // with two workgroups sharing a CU its copy of the chase competes for the other's SIMDs
     // (3s5z K = 5, 512 trees: +0.5 us per launch), so wave 0 gathers there
     const bool w1g = kTreeW1Gather<NC> && (fast_ok & 2) != 0;
+    // the level-walk classes with one workgroup per CU: wave 0 hands the leaf's parent over through
+    // LDS (xi[56]: 0 pending, index + 1, or -1 for none) and wave 1 gathers the row, in parallel
+    // with wave 0's epilogue
+#ifdef MZ_NO_LVG
+    constexpr bool lvg = false;
+#else
+    const bool lvg = SEL && kTreeLevels<NC> && pool != nullptr && (fast_ok & 2) != 0;
+#endif
     const int B = BA & 0xffffff, A = (int)((unsigned)BA >> 24);
     const int pe = pk & 0x1ffff, gK = (int)((unsigned)pk >> 17);
     const int ne = (1ll + (long long)gK * (pe - 1)) < P ? 1 + gK * (pe - 1) : P;  // node bound (launch_step)
@@ -5160,6 +5168,43 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 }
             }
         }
+        if (lvg) {
+            // wait for wave 0's walk (LDS-coherent within the workgroup; bounded, and wave 0 writes
+            // the slot on every path after barrier (2))
+            volatile int *slot = (volatile int *)(xi + 56);
+            int v = 0;
+            for (int it = 0; it < (1 << 22); ++it) {
+                v = uni(*slot);
+                if (v != 0) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (v > 0) {  // mcts_sampled.py:130-134: pool[parent's hsx][t]
+                const char *src = pool + (long long)(v - 1) * pool_stride + (long long)t * row_bytes;
+                char *gdst = gather_out + (long long)t * row_bytes;
+                const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool |
+                                  (long long)(uintptr_t)gather_out) & 15) == 0;
+                if (al) {  // sixteen 16-byte loads per lane in flight, then their stores, written through
+                    for (long long o0 = (long long)l * 16; o0 < row_bytes; o0 += 16 * 16 * kWave) {
+                        int4 rv[16];
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) {
+                            const long long o = o0 + (long long)u * 16 * kWave;
+                            if (o < row_bytes) rv[u] = *(const int4 *)(src + o);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 16; ++u) {
+                            const long long o = o0 + (long long)u * 16 * kWave;
+                            if (o < row_bytes) st_wt16(gdst + o, rv[u]);
+                        }
+                    }
+                } else {
+                    for (long long o2 = (long long)l * 4; o2 < row_bytes; o2 += 4 * kWave)
+                        *(int *)(gdst + o2) = *(const int *)(src + o2);
+                }
+            } else if (v == 0 && l == 0) {
+                atomicOr(d.err(), kErrPath);  // (never: wave 0 did not hand over)
+            }
+        }
         wait_vm();  // nothing of this wave may be in flight when the block ends
         return;
     }
@@ -5377,6 +5422,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     rm3 = span_mark();
 #endif
     if (l == 0) {
+        xi[56] = 0;  // (the level-walk classes' row hand-over: pending)
         xi[15] = ncl;
         xi[14] = err;
         xi[58] = cursor;  // the selection's first engine word, for wave 1's copy of the chase
@@ -5560,10 +5606,11 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     // the leaf's hidden-state row (mcts_sampled.py:130-134): pool[idx_x][t].  Rows up to 16 KiB go
     // through LDS-DMA into the value-entry area (free once wave 1 is done), so nothing waits for
     // them until the copy-out at the very end
+    if (lvg && l == 0) *(volatile int *)(xi + 56) = err ? -1 : out_idx + 1;  // (wave 1 gathers)
     bool gath_lds = false;
     char *gdst = nullptr;
     unsigned char *sbig = smem + L::oReg;
-    if (SEL && !w1g && pool && !err) {
+    if (SEL && !w1g && !lvg && pool && !err) {
         const char *src = pool + (long long)out_idx * pool_stride + (long long)t * row_bytes;
         gdst = gather_out + (long long)t * row_bytes;
         const bool al = ((row_bytes | pool_stride | (long long)(uintptr_t)pool | (long long)(uintptr_t)gather_out) &
