@@ -4991,7 +4991,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         if (SEL && !kTreeLevels<NC> && wv < 4) {
             const int ncl = uni(xi[15]), err = bk_err<NC>(smem) | uni(xi[14]);
             tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, gdel, PS, D);
-            if (wv == 2 && w1g && pool && !err) {
+            if (wv == 2 && !err) {  // (every fused launch of the precomputed classes: see wave 0's header)
                 // where wave 1 gathers the row and writes the path record, this wave runs a third
                 // copy of the chase and writes the header but its tame flag (wave 0's), so that wave
                 // 0's epilogue is the selection outputs and the counters
@@ -5658,7 +5658,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #ifdef MZ_SPANS_EPI
     rm2 = span_mark();
 #endif
-    if (w1path && !err) {  // (wave 2 writes the rest of the header)
+    if (SEL && !kTreeLevels<NC> && !err) {  // (wave 2 writes the rest of the header)
         if (l == 0) d.hdr()[t].tame = h.tame;
     } else {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
         const int cur = err ? h.cursor : cursor;
