@@ -1,4 +1,4 @@
-"""Multi-rank root sharding on CPU (gloo, world_size 2): each rank searches its contiguous shard
+"""Multi-rank root sharding on CPU (gloo, world_size 2 and 4): each rank searches its contiguous shard
 of the roots with root_offset; gathered results are bit-identical to one unsharded batch.  Uses
 the CPU port as the tree backend, so it runs anywhere; the GPU variant is in test_gpu_parity.py."""
 from __future__ import annotations
@@ -68,13 +68,14 @@ def test_shard_bounds():
             assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
 
 
-@pytest.mark.parametrize("K", [1, 5])
-def test_gloo_two_ranks_match_unsharded(K):
+@pytest.mark.parametrize("world,K", [(2, 1), (2, 5), (4, 5)])
+def test_gloo_ranks_match_unsharded(world, K):
+    """world 4 rehearses a wider job on the CPU: 37 roots split 10/9/9/9 (ragged shards)."""
     _ensure_oracle_built()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 37, K, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 37, K, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
