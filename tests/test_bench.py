@@ -80,6 +80,28 @@ def test_gpus_flag_spawns_ranks(port_lib):
     assert line["strong_scaling"]["roots_total"] == 8
 
 
+def test_gpus_flag_eight_ranks(port_lib):
+    """The driver's widest job, rehearsed on the CPU: `bench.py --gpus 8` over gloo with the port
+    backend, the metric's 256 roots split 32 per rank; rank 0 prints one line naming 8 ranks."""
+    import json
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "port", "--sims", "4",
+           "--steps", "1", "--warmup", "1", "--no-cpu"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8 and line["config"]["roots_total"] == 256 and line["config"]["roots_per_gpu"] == 32
+    rk = line["ranks"]
+    assert rk["world_size"] == 8 and [x["rank"] for x in rk["per_rank"]] == list(range(8))
+    assert abs(max(x["ms_per_step"]["strong"] for x in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
+
+
 def test_strong_leg_is_the_global_batch(port_lib):
     """The strong leg's ranks search slices of ONE global batch: rank r's inputs are rows [lo, hi)
     of the inputs an unsharded run generates (so N > 1 measures the metric's own job)."""
