@@ -85,6 +85,12 @@ def parse(argv=None):
     ap.add_argument("--dropin", action="store_true",
                     help="time the tree-level drop-in instead: the reference driver's host loop "
                          "(mcts_sampled.py:114-172, numpy in and out of every Tree_batch call) on mazero_amd.cytree")
+    ap.add_argument("--broadcast-every", type=int, default=0, metavar="N",
+                    help="BASELINE config #5's weight broadcast: every N env steps inside the timed loop, rank 0 "
+                         "publishes a new checkpoint and every rank runs WeightBroadcaster.sync() of the "
+                         "--broadcast-map network's flat weights (selfplay_worker.py:371-375); 0 = off")
+    ap.add_argument("--broadcast-map", default="27m_vs_30m", choices=sorted(CONFIGS),
+                    help="the map whose network's weights the broadcast carries (config #5: 27m_vs_30m)")
     ap.add_argument("--backend", default="hip", choices=("hip", "port"),
                     help="'port': every rank searches on the host with the CPU port over gloo -- a CPU "
                          "test of the launcher / sharding / clock plumbing only, never a measurement")
@@ -204,11 +210,13 @@ class HipLeg:
     def stats(self):
         return [sd["tb"].stats() for sd in self.searches]
 
-    def run(self, steps):
+    def run(self, steps, before_step=None):
         import torch
 
         with torch.cuda.stream(self.stream):
-            for _ in range(steps):
+            for i in range(steps):
+                if before_step is not None:
+                    before_step(i)
                 if self.graph is not None:
                     self.graph.replay()
                 else:
@@ -414,8 +422,10 @@ class DropinLeg:
     def check(self):
         pass
 
-    def run(self, steps):
-        for _ in range(steps):
+    def run(self, steps, before_step=None):
+        for i in range(steps):
+            if before_step is not None:
+                before_step(i)
             self.env_step()
 
 
@@ -455,9 +465,62 @@ class PortLeg:
     def check(self):
         pass
 
-    def run(self, steps):
-        for _ in range(steps):
+    def run(self, steps, before_step=None):
+        for i in range(steps):
+            if before_step is not None:
+                before_step(i)
             self.env_step()
+
+
+class WeightSync:
+    """--broadcast-every N (BASELINE config #5, "self-play shard + RCCL weight broadcast"): before
+    every N-th env step of the timed loop rank 0 publishes a new checkpoint index and every rank runs
+    WeightBroadcaster.sync() (mazero_amd/weights.py): the index, then the --broadcast-map network's
+    flat weights (one message per dtype) over the job's collective (RCCL on GPUs, gloo for
+    --backend port), replacing the reference's Ray pull before an env step
+    (selfplay_worker.py:371-375, storage.py:68-80).  checkpoint_interval 1, so every sync moves the
+    weights.  Each rank times its own syncs on the host, the collective completed
+    (stream-synchronised); the search graphs run on their own stream, which waits for the weights
+    before the next env step."""
+
+    def __init__(self, args, dev, stream=None):
+        import torch.distributed as dist
+
+        from mazero_amd.nets import make_net
+        from mazero_amd.weights import WeightBroadcaster
+
+        N, A = CONFIGS[args.broadcast_map]
+        self.every, self.dev, self.stream = args.broadcast_every, dev, stream
+        self.rank = dist.get_rank()
+        self.net = make_net(N, A, seed=11 + self.rank, device=dev)  # different weights on every rank
+        self.wb = WeightBroadcaster(self.net, src=0)
+        self.bytes = sum(t.numel() * t.element_size() for t in self.wb.flat.tensors())
+        self.index, self.calls, self.secs = 0, 0, 0.0
+
+    def __call__(self, step):
+        if step % self.every:
+            return
+        import torch
+
+        t0 = time.perf_counter()
+        if self.rank == 0:
+            self.index += 1
+            self.wb.publish(self.index)
+        got = self.wb.sync()
+        if self.dev.type == "cuda":
+            cur = torch.cuda.current_stream(self.dev)
+            cur.synchronize()
+        self.secs += time.perf_counter() - t0
+        self.calls += 1
+        if got != self.index and self.rank == 0:
+            raise RuntimeError(f"weight broadcast: sync returned checkpoint {got}, published {self.index}")
+
+    def reset(self):
+        self.calls, self.secs = 0, 0.0
+
+    def record(self):
+        return dict(syncs=self.calls, ms_per_sync=round(self.secs / max(1, self.calls) * 1e3, 4),
+                    checkpoint=int(self.wb.model_index), transfers=int(self.wb.syncs))
 
 
 def trace_mark(dev, k):
@@ -471,15 +534,16 @@ def trace_mark(dev, k):
     torch.full((1,), k, dtype=torch.int16, device=dev)
 
 
-def timed(leg, steps, world, dist, sync, dev):
+def timed(leg, steps, world, dist, sync, dev, before_step=None):
     """EXACTLY `steps` env steps between barrier + device synchronisation on both sides; the max
-    over ranks of the wall time, and this rank's own."""
+    over ranks of the wall time, and this rank's own.  `before_step(i)` (the weight broadcast of
+    --broadcast-every) runs inside the timed region."""
     trace_mark(dev, 1)
     if world > 1:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    leg.run(steps)
+    leg.run(steps, before_step)
     sync()
     elapsed = time.perf_counter() - t0
     own = elapsed
@@ -508,6 +572,9 @@ def rank_record(rank, local, dev, legs, steps):
         if bus is not None:
             rec["pci_bus_id"] = int(bus)
     rec["ms_per_step"] = {k: round(v["own"] / steps * 1e3, 4) for k, v in legs.items()}
+    bc = {k: v["broadcast"] for k, v in legs.items() if v.get("broadcast")}
+    if bc:
+        rec["weight_broadcast"] = bc
     return rec
 
 
@@ -556,6 +623,18 @@ def main():
         rank = dist.get_rank()
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has {world} rank(s)")
+    if args.broadcast_every < 0:
+        raise SystemExit("bench.py: --broadcast-every must be >= 0")
+    if args.broadcast_every and not dist.is_initialized():
+        # one rank: a single-rank group, so that the broadcast runs the same collective code path
+        import socket
+
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        kw = dict(device_id=dev) if hip else {}
+        dist.init_process_group("nccl" if hip else "gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, **kw)
     sync = torch.cuda.synchronize if hip else (lambda: None)
     N, A = CONFIGS[args.map]
     S, K = args.sims, args.sampled_times
@@ -596,10 +675,16 @@ def main():
                 inputs = [slice_inputs(inp, lo, hi) for inp in inputs]
         leg = make_leg(inputs, off)
         leg.prepare()
+        wsync = None
+        if args.broadcast_every:
+            wsync = WeightSync(args, dev, stream if hip else None)
+            wsync(0)  # (warm-up: the first sync allocates the collective's buffers)
+            wsync.reset()
         st0 = leg.stats() if hip and rank == 0 and not args.dropin else None
-        elapsed, own = timed(leg, args.steps, world, dist, sync, dev)
+        elapsed, own = timed(leg, args.steps, world, dist, sync, dev, wsync)
         st1 = leg.stats() if hip and rank == 0 and not args.dropin else None
-        legs[kind] = dict(leg=leg, B=B, total=total, elapsed=elapsed, own=own, st0=st0, st1=st1)
+        legs[kind] = dict(kind=kind, leg=leg, B=B, total=total, elapsed=elapsed, own=own, st0=st0, st1=st1,
+                          broadcast=None if wsync is None else wsync.record(), wsync=wsync)
     # N > 1: every rank's device and its own step time, gathered to rank 0, and the collective's
     # view of the job (the line checks itself against the launcher's world size)
     ranks = None
@@ -673,13 +758,25 @@ def main():
             },
             **other,
             **({"ranks": ranks} if ranks is not None else {}),
+            **({"weight_broadcast": weight_broadcast_line(args, m, ranks)} if args.broadcast_every else {}),
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+
+
+def weight_broadcast_line(args, m, ranks):
+    """The --broadcast-every fields of the line: what moved and each rank's own time per sync in the
+    headline leg (rank 0's own beside them)."""
+    rec = dict(every_steps=args.broadcast_every, network=f"{args.broadcast_map} MuZero-shaped (mazero_amd.nets)",
+               bytes=m["wsync"].bytes, src_rank=0, checkpoint_interval=1, **m["broadcast"])
+    if ranks is not None:
+        rec["per_rank_ms_per_sync"] = [r.get("weight_broadcast", {}).get(m["kind"], {}).get("ms_per_sync")
+                                       for r in ranks["per_rank"]]
+    return rec
 
 
 def workload_key(args):

@@ -126,11 +126,29 @@ int mz_fused_kernel(mz_batch *b, char *out, int len);
 
 /* Release what the library keeps for reuse across handles: device arenas of destroyed handles
  * (at most 2 GiB / 16 blocks per process, reused by a handle of the same size, as the reference's
- * per-search Tree_batch re-creates them, mcts_sampled.py:89) and pinned host stages (at most
- * 256 MiB).  The per-device mt19937 seeding table (~97 MB, built at the first mz_create on a
- * device) stays.  `released` (may be NULL) receives the bytes freed.  A handle's own arena is
- * never touched; an arena allocation that fails releases the cache and retries by itself. */
+ * per-search Tree_batch re-creates them, mcts_sampled.py:89), pinned host stages (at most
+ * 256 MiB) and the per-device mt19937 seeding tables (~97 MB each, built at the first mz_create on
+ * a device) of every device with no live handle (the next mz_create there builds it again, a few
+ * ms).  `released` (may be NULL) receives the bytes freed.  A handle's own arena is never
+ * touched; an arena allocation that fails releases the cache and retries by itself. */
 int mz_trim_caches(int64_t *released);
+
+/* Device memory of a handle (sizing against the 288 GB of HBM; diagnostics): up to n of
+ * {the arena's bytes, the pUCT coefficient tables' (T, pb, sq), the value entries' (B P (S + 1)
+ * entries of 8 bytes), the engine streams' (B W words), the node records'} into out. */
+int mz_arena_info(mz_batch *b, int64_t *out, int n);
+
+/* Diagnostics (tests): the selection state each tree carries into its next launch, copied to host
+ * memory after the handle's queued work.  In the k_tree classes with a precomputed chase three
+ * waves chase the same LDS state: wave 0 writes the selection outputs (idx_x, actions), wave 1 the
+ * path record the next back-propagation reads (one workgroup per CU) and wave 2 the header; this
+ * returns the last two so that a test can check them against the first.
+ *   header [B][6]: cursor (the next engine word), nodes, path length D, error bits, leaf, tame;
+ *   path [B][max_levels][4]: path level i <= min(D, max_levels - 1) as {node, visits at selection,
+ *   the node's hidden_state_index_x, the action on the edge into the node (-1 at the root)};
+ *   levels past D are -1.  K = 1 chain kernels (k_chain3, k_chain) keep no path record: their
+ *   path entries are -1 past level 0. */
+int mz_debug_paths(mz_batch *b, int32_t *header, int32_t *path, int max_levels);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,9 @@
 extern "C" {
 #endif
 
-#define MZ_ABI_VERSION 1
+/* 2 (round 6): MZ_S_RNG_TIE_BEYOND / MZ_S_RNG_NXT_BEYOND inserted at 10 and 11, the stamp slots
+ * moved up by two, MZ_S_COUNT 32 */
+#define MZ_ABI_VERSION 2
 
 typedef struct mz_batch mz_batch;
 
@@ -79,32 +81,37 @@ enum mz_stat {
                               * or max, CMinMaxStats utils.cpp:79-103) differs from before:
                               * every internal node's select_child outcome may change then
                               * (counted by k_tree, k_step and k_hbm; 0 for the K = 1 chains)  */
+    MZ_S_RNG_TIE_BEYOND = 10,/* tie draws (gen() % size, cnode.cpp:373-377) whose engine word
+                              * lies past the launch's LDS window of the tree's stream, read
+                              * from HBM by the selection's chase (k_tree only)              */
+    MZ_S_RNG_NXT_BEYOND = 11,/* launches whose next expansion's engine words (the header's
+                              * copy) lie past that window, read from HBM (k_tree only)      */
     /* Diagnostic builds only (compiled with MZ_STAMPS=1; zero otherwise): shader cycles of the
      * fused simulation-step kernel, summed over trees and launches, read with s_memtime where the
      * wave's instruction stream reaches each point (no forced waits).  Wave 0 (expansion,
      * selection, gather): */
-    MZ_S_CYC_HEADER = 10,     /* round 1: header, tables, network outputs issued and waited   */
-    MZ_S_CYC_STAGE1 = 11,    /* slow-path check (host bounds too small)                    */
-    MZ_S_CYC_STAGE2 = 12,    /* round 2 issue: RNG window, the leaf's record               */
-    MZ_S_CYC_EXPAND = 13,    /* leaf expansion                                             */
-    MZ_S_CYC_BACKUP = 14,    /* waiting for the back-propagation wave (barrier)            */
-    MZ_S_CYC_MINMAX = 15,    /* waiting for the RNG window                                 */
-    MZ_S_CYC_SELECT = 16,    /* value scores + selection walk                              */
-    MZ_S_CYC_GATHER = 17,    /* hidden-state gather loads                                  */
-    MZ_S_CYC_EPILOGUE = 18,  /* header write-back, gather stores, statistics               */
-    MZ_S_STAMPED = 19,       /* stamped launches x trees                                   */
+    MZ_S_CYC_HEADER = 12,     /* round 1: header, tables, network outputs issued and waited   */
+    MZ_S_CYC_STAGE1 = 13,    /* slow-path check (host bounds too small)                    */
+    MZ_S_CYC_STAGE2 = 14,    /* round 2 issue: RNG window, the leaf's record               */
+    MZ_S_CYC_EXPAND = 15,    /* leaf expansion                                             */
+    MZ_S_CYC_BACKUP = 16,    /* waiting for the back-propagation wave (barrier)            */
+    MZ_S_CYC_MINMAX = 17,    /* waiting for the RNG window                                 */
+    MZ_S_CYC_SELECT = 18,    /* value scores + selection walk                              */
+    MZ_S_CYC_GATHER = 19,    /* hidden-state gather loads                                  */
+    MZ_S_CYC_EPILOGUE = 20,  /* header write-back, gather stores, statistics               */
+    MZ_S_STAMPED = 21,       /* stamped launches x trees                                   */
     /* wave 1 (back-propagation): */
-    MZ_S_CYC_W1_ROUND1 = 20, /* round 1: node records, path, lambda powers issued and waited */
-    MZ_S_CYC_W1_STAGE2 = 21, /* round 2 issue: path-node value sets, value entries         */
-    MZ_S_CYC_W1_BACKUP = 22, /* back-propagation + min/max                                 */
-    MZ_S_CYC_W1_SYNC = 23,   /* wave 1's whole span, start to back-propagation done        */
-    MZ_S_CYC_EXP_CDF = 24,   /* expansion: sampling distribution                           */
-    MZ_S_CYC_EXP_DRAW = 25,  /* expansion: K draws                                         */
-    MZ_S_CYC_EXP_NODES = 26, /* expansion: child creation                                  */
-    MZ_S_CYC_BAK_BOOT = 27,  /* back-propagation: bootstrap values                         */
-    MZ_S_CYC_BAK_WAIT = 28,  /* back-propagation: waiting for staged entries               */
-    MZ_S_CYC_BAK_NODES = 29, /* back-propagation: node updates                             */
-    MZ_S_COUNT = 30
+    MZ_S_CYC_W1_ROUND1 = 22, /* round 1: node records, path, lambda powers issued and waited */
+    MZ_S_CYC_W1_STAGE2 = 23, /* round 2 issue: path-node value sets, value entries         */
+    MZ_S_CYC_W1_BACKUP = 24, /* back-propagation + min/max                                 */
+    MZ_S_CYC_W1_SYNC = 25,   /* wave 1's whole span, start to back-propagation done        */
+    MZ_S_CYC_EXP_CDF = 26,   /* expansion: sampling distribution                           */
+    MZ_S_CYC_EXP_DRAW = 27,  /* expansion: K draws                                         */
+    MZ_S_CYC_EXP_NODES = 28, /* expansion: child creation                                  */
+    MZ_S_CYC_BAK_BOOT = 29,  /* back-propagation: bootstrap values                         */
+    MZ_S_CYC_BAK_WAIT = 30,  /* back-propagation: waiting for staged entries               */
+    MZ_S_CYC_BAK_NODES = 31, /* back-propagation: node updates                             */
+    MZ_S_COUNT = 32
 };
 
 /* --- library -------------------------------------------------------------------------- */
@@ -216,7 +223,8 @@ typedef struct {
 int mz_get_roots_device(mz_batch *b, float discount, const mz_readback_out *out);
 
 /* --- diagnostics ----------------------------------------------------------------------- */
-/* Counters accumulated since creation (MZ_S_COUNT int64 values); host memory. */
+/* Counters accumulated since creation (MZ_S_COUNT int64 values of this header's ABI: size the buffer
+ * by the MZ_S_COUNT of the MZ_ABI_VERSION that mz_abi_version() returns); host memory. */
 int mz_get_stats(mz_batch *b, int64_t *out);
 /* CTree_batch::print (cnode.cpp:783-791): debug dump to stderr. */
 int mz_print(mz_batch *b);

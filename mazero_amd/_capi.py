@@ -51,6 +51,8 @@ STATS = [
     "entries_written",
     "minmax_nodes",
     "mm_moved",
+    "rng_tie_beyond",
+    "rng_nxt_beyond",
     "cyc_header",
     "cyc_stage1",
     "cyc_stage2",
@@ -118,6 +120,8 @@ DRIVER_SIGNATURES = {
     "mz_expand_backup_readback": (_i, [_p, _i, _f, _i, _p, _p, _p, _p, _f, _p]),
     "mz_readback_ready": (_i, [_p, _f]),
     "mz_trim_caches": (_i, [C.POINTER(_i64)]),
+    "mz_debug_paths": (_i, [_p, _p, _p, _i]),
+    "mz_arena_info": (_i, [_p, _p, _i]),
 }
 DRIVER_EXPORTS = sorted(DRIVER_SIGNATURES)
 

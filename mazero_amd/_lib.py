@@ -13,6 +13,7 @@ import threading
 from . import _capi
 from .build import LIB, LIB_STAMPS
 
+ABI = 2  # MZ_ABI_VERSION of include/mzmcts.h
 _lock = threading.Lock()
 _lib = None
 
@@ -37,8 +38,8 @@ def load() -> C.CDLL:
                 "or __graft_entry__.build())"
             )
         lib = _capi.bind(C.CDLL(path, mode=C.RTLD_LOCAL))
-        if lib.mz_abi_version() != 1 or lib.mz_backend() != b"hip-gfx950":
-            raise RuntimeError(f"{path} is not the hip-gfx950 backend of ABI 1")
+        if lib.mz_abi_version() != ABI or lib.mz_backend() != b"hip-gfx950":
+            raise RuntimeError(f"{path} is not the hip-gfx950 backend of ABI {ABI}")
         _lib = lib
         return lib
 

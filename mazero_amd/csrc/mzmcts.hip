@@ -60,6 +60,8 @@ constexpr int kMaxActions = 64;  // one lane per action
 constexpr int kMtN = 624;
 constexpr int kTableLdsMax = 48 * 1024;  // the pUCT table is staged in LDS when it fits this
 constexpr int kNxt = 32;  // RNG words for the next expansion carried in the tree header (2K <= kNxt)
+// the kernels stage a tree's counters as 2 * MZ_S_COUNT dwords, one per lane
+static_assert(2 * MZ_S_COUNT <= 64, "statistics staging: one dword per lane");
 
 enum : int {
     kErrPool = 1,      // node pool exhausted (more expansions than simulation_num allows)
@@ -193,8 +195,17 @@ __host__ __device__ __forceinline__ void arena_nodes(Dev &d, unsigned B, unsigne
     d.o_C = d.o_PP + s4;
     d.o_hdr = d.o_C + s16;
 }
+// pUCT coefficient table entries, T[n (n + 1) / 2 + v] = pb_c(n, v) for n < PS, padded to 4.  Only
+// k_step's LDS-staged table (4 TT <= kTableLdsMax: PS <= 155) and the k_tree level-walk classes
+// (value entries E <= kBkCap: PS <= 342) read past T[0]; every other kernel computes pb_c from the
+// per-n pb / sq tables with the same double arithmetic.  Past kTableFullPS the table is T[0] alone,
+// O(S) instead of O(S^2) on host and device (S = 65,000 would need 8.5 GB).
+constexpr unsigned kTableFullPS = 512;
+__host__ __device__ __forceinline__ unsigned table_entries(unsigned PS) {
+    return PS <= kTableFullPS ? ((PS * (PS + 1) / 2) + 3) & ~3u : 4u;
+}
 __host__ __device__ __forceinline__ void arena_hot(Dev &d, unsigned B, unsigned P, unsigned PS) {
-    const unsigned TT = ((PS * (PS + 1) / 2) + 3) & ~3u;
+    const unsigned TT = table_entries(PS);
     arena_nodes(d, B, P);
     unsigned o = d.o_hdr;
     o += (B * (unsigned)sizeof(TreeHdr) + 64 + 255) / 256;
@@ -4038,6 +4049,7 @@ constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : (NC >= 1024 ? MZ_TREE_BK1024 : M
 template <int NC>
 constexpr int kTreeWavesN = kBkN<NC> + 1;
 constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
+static_assert(kBkCap + 2 <= (int)kTableFullPS, "the k_tree level walk reads the full pUCT table");
 // the 512-node class with seven back-propagation waves keeps two workgroups per CU (76 KB of LDS
 // each) with slots of 128 entries (S + 1 <= 128; larger searches take k_step); so does kTree1024S
 template <int NC>
@@ -4660,7 +4672,8 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
 // wave 1 runs the same chase on the same LDS state for the leaf's parent only, and gathers its row.
 template <int NC, bool REC>
 __device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, int t, int gW, int wbase, int wsh,
-                                           int PS, int &cursor, int &err, int &Dn, int &x, int &xprev, int &px) {
+                                           int PS, int &cursor, int &err, int &Dn, int &x, int &xprev, int &px,
+                                           int &nbw) {
     using L = TreeLayout<NC>;
     const int l = lane_id();
     const int4 *sA = (const int4 *)(smem + L::oA);
@@ -4721,6 +4734,7 @@ __device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, in
                 }
                 const unsigned lo = (unsigned)uni(f2i(rb.x)), hi = (unsigned)uni(f2i(rb.y));
                 if (cnt > 1) {
+                    if (!inwin) ++nbw;  // (MZ_S_RNG_TIE_BEYOND)
                     const unsigned w = inwin ? (unsigned)uni((int)wwin) : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
                     const int k = uni((int)(w % (unsigned)cnt));
                     const unsigned lst_l = (l < 32) ? (lo >> l) : (hi >> (l - 32));
@@ -4997,8 +5011,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 // 0's epilogue is the selection outputs and the counters
                 const int gW2 = pl->g.W;
                 d.o_R = pl->d.o_R;
-                int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0, e = 0;
-                tree_chase<NC, false>(smem, d, t, gW2, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px);
+                int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0, e = 0, nbw = 0;
+                tree_chase<NC, false>(smem, d, t, gW2, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px, nbw);
                 if (!e) {
                     TreeHdr *hp = d.hdr() + t;
                     const int wb = uni(xi[62]), ws = uni(xi[59]);
@@ -5116,8 +5130,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 // this wave's copy of wave 0's chase; while the row's loads are in flight, the path
                 // record {node, visits at selection} for the next back-propagation and the scored
                 // children's count (wave 0's epilogue leaves both to this wave)
-                int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0;
-                tree_chase<NC, true>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px);
+                int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0, nbw = 0;
+                tree_chase<NC, true>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px, nbw);
                 auto write_path = [&]() {
                     int2 *gp = d.path() + (size_t)t * PS;
                     const int2 *sPath1 = (const int2 *)(smem + L::oPath);
@@ -5462,6 +5476,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     unsigned long long tp[4] = {0};
     int Dn = 0, x = 0, out_idx = 0, out_act = 0;
     long long nscored = 0;
+    int nbeyond = 0, nxbeyond = 0;  // engine words read past the LDS window: ties, header words
     int px = 0, pvv = 0;  // level i's node (and, by levels, its visits) in lane i; sPath past 64 levels
     if constexpr (!SEL) {
         stamp(ts, 5);
@@ -5554,6 +5569,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                     }
                     if (cntl > 1) {
                         const int o = cursor - wbase + wsh;
+                        if (!(o >= wsh && o < kRngWin)) ++nbeyond;
                         const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
                                                                    : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
                         for (int k = uni((int)(w % (unsigned)cntl)); k > 0; --k) lst &= lst - 1ull;
@@ -5589,7 +5605,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         stamp(ts, 5);
     if (!err) {
         int xprev = 0;
-        tree_chase<NC, true>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px);
+        tree_chase<NC, true>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px, nbeyond);
         out_idx = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
         out_act = act_of(uni(sB[x].y));            // children_action of the last edge
     }
@@ -5660,6 +5676,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #endif
     if (SEL && !kTreeLevels<NC> && !err) {  // (wave 2 writes the rest of the header)
         if (l == 0) d.hdr()[t].tame = h.tame;
+        const int o0 = cursor - wbase + wsh;  // (wave 2's fetch past the window, counted here)
+        if (!(o0 >= wsh && o0 + kNxt <= kRngWin)) nxbeyond = 1;
     } else {  // the header: scalars from lane 0, the next expansion's engine words from lanes 0..kNxt-1
         const int cur = err ? h.cursor : cursor;
         const int o0 = cur - wbase + wsh;
@@ -5667,6 +5685,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         if (uni((int)(o0 >= wsh && o0 + kNxt <= kRngWin))) {
             if (l < kNxt) hp->nxt[l] = sRng[o0 + l];
         } else {  // beyond the window (rare): through LDS-DMA (no compiler wait on the row's loads)
+            nxbeyond = 1;
             unsigned *scr = (unsigned *)(smem + L::oIx);
             const int w = cur + l < gW ? cur + l : gW - 1;
             glds4a(d.R() + (size_t)t * gW + w, scr);
@@ -5739,6 +5758,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         add = sel_lane(add, ent_w, 1ull << MZ_S_ENTRIES_WRITTEN);
         add = sel_lane(add, (long long)(tot - 1), 1ull << MZ_S_MINMAX_NODES);
         add = sel_lane(add, (long long)moved, 1ull << MZ_S_MM_MOVED);
+        add = sel_lane(add, (long long)nbeyond, 1ull << MZ_S_RNG_TIE_BEYOND);
+        add = sel_lane(add, (long long)nxbeyond, 1ull << MZ_S_RNG_NXT_BEYOND);
         if (MZ_STAMPS) switch (l) {
             case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;    // round 1
             case MZ_S_CYC_STAGE2: add = (long long)(ts[2] - ts[1]); break;    // barrier (1) wait
@@ -5945,6 +5966,9 @@ struct mz_batch {
     int chain3_nc = 0;         // k_chain3 node class (64 .. 1024) for K = 1 trees, 0: k_chain / k_step
     int tree_nc = -1;          // k_tree node class for 2 <= K <= 64 trees (-1: k_step)
     bool hbm = false;          // the pool's LDS image exceeds a CU's LDS: every step launch is k_hbm
+    bool seed_ref = false;     // holds a reference on its device's seeding table (seed_table)
+    // device bytes by kind (mz_arena_info): pUCT tables, value entries, engine streams, node records
+    size_t mem_tables = 0, mem_values = 0, mem_stream = 0, mem_nodes = 0;
     Params *prm = nullptr;     // device copy of {geo, dev} (in the arena)
     // Host-memory path (the cytree numpy surface): one pinned stage per handle, laid out
     // [inputs B*(2+3NA) | selection B*(2+N) | error word | packed readback rb_words] (4-byte words).
@@ -5989,11 +6013,15 @@ int round16(int x) { return (x + 15) & ~15; }
 // of the device: rows for every seed value v = random_seed * 2333 + root index (cnode.cpp:574) below
 // its size, sized for random_seed < 256 (np_random.choice(256), mcts_sampled.py:89) and at least
 // 4096 roots (~97 MB).  Built once (a few ms), grown when a handle's roots need more; an outgrown
-// table stays allocated (handles made before it, and graphs they recorded, read it).  Seeds outside
-// the table take the sequential chain.
+// table stays allocated while handles made before it (and graphs they recorded) may read it.  Every
+// live handle holding a table counts in `live`; mz_trim_caches frees a device's tables when none
+// does.  Seeds outside the table take the sequential chain.
 struct SeedTable {
     unsigned *p = nullptr;
     unsigned n = 0;
+    int live = 0;                // live handles that read this device's tables
+    std::vector<void *> old;     // outgrown tables
+    size_t bytes = 0;            // of p and old together
 };
 constexpr int kSeedTabDevices = 64;
 std::mutex g_seed_mu;
@@ -6024,11 +6052,34 @@ void seed_table(int dev, unsigned long long need, const unsigned **cp, unsigned 
             (void)hipGetLastError();
             return;
         }
+        if (st.p) st.old.push_back(st.p);
         st.p = (unsigned *)p;
         st.n = (unsigned)n;
+        st.bytes += (size_t)n * kSeedRow * sizeof(unsigned);
     }
     *cp = st.p;
     *cp_n = st.n;
+    ++st.live;
+}
+
+void seed_table_release(int dev) {
+    if (dev < 0 || dev >= kSeedTabDevices) return;
+    std::lock_guard<std::mutex> lk(g_seed_mu);
+    if (g_seed_tab[dev].live > 0) --g_seed_tab[dev].live;
+}
+
+// the tables of every device no live handle reads; returns the bytes freed
+size_t seed_table_trim() {
+    std::lock_guard<std::mutex> lk(g_seed_mu);
+    size_t freed = 0;
+    for (SeedTable &st : g_seed_tab) {
+        if (st.live > 0 || !st.p) continue;
+        (void)hipFree(st.p);
+        for (void *q : st.old) (void)hipFree(q);
+        freed += st.bytes;
+        st = SeedTable{};
+    }
+    return freed;
 }
 
 // A non-blocking stream per device for mz_create's initialisation launch (never captured, so a
@@ -6172,9 +6223,11 @@ int ensure_tables(mz_batch *b, float c2, float c1) {
         sq[n] = ::sqrt((double)n);
     }
     // pb_c(n, v) for every parent total n and child visits v <= n, with ucb_score's operations:
-    // pb_c = pb[n]; pb_c *= (sqrt(n) / (v + 1))   (float *= double)
+    // pb_c = pb[n]; pb_c *= (sqrt(n) / (v + 1))   (float *= double); past kTableFullPS only T[0]
+    // (table_entries)
     std::vector<float> T(b->geo.TT, 0.f);
-    for (int n = 0; n < b->PS; ++n)
+    const int tn = b->PS <= (int)kTableFullPS ? b->PS : 1;
+    for (int n = 0; n < tn; ++n)
         for (int v = 0; v <= n; ++v) {
             float pbc = pb[n];
             pbc = (float)((double)pbc * (sq[n] / (double)(v + 1)));
@@ -6758,8 +6811,8 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         if (cap < S + 1) cap = S + 1;
         g.reg_cap = (int)cap;
     }
-    g.TT = ((g.PS * (g.PS + 1) / 2) + 3) & ~3;
-    g.use_table = (4 * g.TT <= kTableLdsMax) ? 1 : 0;
+    g.TT = (int)table_entries((unsigned)g.PS);
+    g.use_table = (g.PS <= (int)kTableFullPS && 4ll * g.TT <= kTableLdsMax) ? 1 : 0;
 #ifdef MZ_NO_TABLE
     g.use_table = 0;
 #endif
@@ -6880,6 +6933,11 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
         plan.dev<int2>(d.o_V, nodes * b->E);
         plan.dev<unsigned>(d.o_R, (size_t)B * b->W);
         plan.dev<float4>(d.o_D, nodes);
+        b->mem_tables = ArenaPlan::span(4 * ((size_t)g.TT + 4 * kWave)) + ArenaPlan::span(4 * ((size_t)b->PS + kWave)) +
+                        ArenaPlan::span(8 * ((size_t)b->PS + kWave));
+        b->mem_values = ArenaPlan::span(8 * nodes * b->E);
+        b->mem_stream = ArenaPlan::span(4 * (size_t)B * b->W);
+        b->mem_nodes = 4 * ArenaPlan::span(16 * nodes) + 3 * ArenaPlan::span(4 * nodes);
         plan.ptr(&b->sel_dev, (size_t)B * (2 + N));
         plan.ptr(&b->in_dev, (size_t)B * (2 + 3 * (size_t)N * A));
         b->rb_words = (size_t)2 * B + 2 * (size_t)B * N * A + (size_t)MZ_F_COUNT * B * b->Wd * N;
@@ -6913,6 +6971,7 @@ int mz_create(int B, int N, int A, int K, int S, float delta_lb, uint32_t seed, 
     if (!getenv_flag("MZ_NO_SEED_TABLE"))
         seed_table(b->device, 255ull * 2333ull + (unsigned long long)(root_offset > 0 ? root_offset : 0) + (unsigned long long)B,
                    &seed_cp, &seed_cp_n);
+    b->seed_ref = seed_cp != nullptr;
     const Params host_params{b->geo, b->dev, seed_cp, seed_cp_n};
     {
         // one launch on the device's init stream, waited for here (the handle's stream is bound later)
@@ -6998,6 +7057,7 @@ int mz_destroy(mz_batch *b) {
         (void)hipHostFree(b->stage);
     if (b->order_ev) (void)hipEventDestroy(b->order_ev);
     if (b->st_ev) (void)hipEventDestroy(b->st_ev);
+    if (b->seed_ref) seed_table_release(b->device);
     delete b;
     return MZ_OK;
 }
@@ -7289,7 +7349,7 @@ int mz_fused_kernel(mz_batch *b, char *out, int len) {
 }
 
 int mz_trim_caches(int64_t *released) {
-    const size_t n = arena_cache().drain(-1, false) + stage_cache().drain(-1, true);
+    const size_t n = arena_cache().drain(-1, false) + stage_cache().drain(-1, true) + seed_table_trim();
     if (released) *released = (int64_t)n;
     return MZ_OK;
 }
@@ -7591,6 +7651,54 @@ int mz_get_stats(mz_batch *b, int64_t *out) {
     for (int k = 0; k < MZ_S_COUNT; ++k) out[k] = 0;
     for (int t = 0; t < b->B; ++t)
         for (int k = 0; k < MZ_S_COUNT; ++k) out[k] += st[(size_t)t * MZ_S_COUNT + k];
+    return MZ_OK;
+}
+
+int mz_arena_info(mz_batch *b, int64_t *out, int n) {
+    if (!b || !out || n < 0) return fail(MZ_ERR_ARG, "mz_arena_info: bad argument");
+    const int64_t v[5] = {(int64_t)b->arena_bytes, (int64_t)b->mem_tables, (int64_t)b->mem_values,
+                          (int64_t)b->mem_stream, (int64_t)b->mem_nodes};
+    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+    return MZ_OK;
+}
+
+int mz_debug_paths(mz_batch *b, int32_t *header, int32_t *path, int max_levels) {
+    if (!b || !header || !path || max_levels < 1) return fail(MZ_ERR_ARG, "mz_debug_paths: bad argument");
+    int rc = ensure_device(b);
+    if (rc) return rc;
+    rc = flush_pending(b);
+    if (rc) return rc;
+    std::vector<TreeHdr> h(b->B);
+    std::vector<int2> pr((size_t)b->B * b->PS);
+    std::vector<int4> bn((size_t)b->B * b->P);
+    HIP_TRY(hipMemcpyAsync(h.data(), b->dev.hdr(), sizeof(TreeHdr) * h.size(), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemcpyAsync(pr.data(), b->dev.path(), sizeof(int2) * pr.size(), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipMemcpyAsync(bn.data(), b->dev.Bn(), sizeof(int4) * bn.size(), hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    const bool chain = !b->hbm && b->chain_nc >= 0;  // (K = 1 chains: no path record)
+    for (int t = 0; t < b->B; ++t) {
+        const TreeHdr &ht = h[t];
+        int32_t *ho = header + (size_t)t * 6;
+        ho[0] = ht.cursor;
+        ho[1] = ht.tot;
+        ho[2] = ht.D;
+        ho[3] = ht.err;
+        ho[4] = ht.leaf;
+        ho[5] = ht.tame;
+        for (int i = 0; i < max_levels; ++i) {
+            int32_t *po = path + ((size_t)t * max_levels + i) * 4;
+            po[0] = po[1] = po[2] = po[3] = -1;
+            if (i > ht.D || i >= b->PS || (chain && i > 0)) continue;
+            const int2 e = pr[(size_t)t * b->PS + i];
+            po[0] = e.x;
+            po[1] = e.y;
+            if (e.x >= 0 && e.x < b->P) {
+                const int4 r = bn[(size_t)t * b->P + e.x];
+                po[2] = r.w;
+                po[3] = i == 0 ? -1 : (r.y >> 8) & 0xff;
+            }
+        }
+    }
     return MZ_OK;
 }
 

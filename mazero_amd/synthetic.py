@@ -141,6 +141,29 @@ def make_search_inputs(
     )
 
 
+def make_deep_window_inputs(rng: np.random.Generator, B: int, S: int, A: int = 2, step: float = 0.2) -> SearchInputs:
+    """Inputs whose searches grow one deep path with a tie at its bottom (round 6, the LDS window of
+    engine words).  Every expansion draws both of A = 2 actions (beta uniform, K large) with priors
+    of ~1e-8, so two unvisited children tie (their prior scores differ by less than the 1e-6 of
+    select_child, cnode.cpp:355-370); rewards rising with the simulation make the visited child's
+    value score the larger one, so each selection walks down the visited chain and draws one word
+    for each level (cnode.cpp:373-377), the tie at the bottom included.  At K = 64 an expansion takes
+    128 words, and at S = 190 the path passes ~130 levels: the selection's and the next expansion's
+    words run past a launch's 256-word LDS window (k_tree's reads from the stream in HBM)."""
+    logits = np.zeros((B, 1, A), np.float32)
+    noises = rng.dirichlet([0.3] * A, B).astype(np.float32).reshape(B, 1, A)
+    seed = int(rng.choice(256))
+    policy, beta, noises = root_preprocess(logits, noises, None, 0.0)
+    sim_policy = np.full((S, B, 1, A), 1e-8, np.float32)
+    sim_beta = np.full((S, B, 1, A), 1.0 / A, np.float32)
+    reward = np.tile((1.0 + step * np.arange(S, dtype=np.float32))[:, None], (1, B)).astype(np.float32)
+    value = np.zeros((S, B), np.float32)
+    return SearchInputs(B=B, A=A, S=S, seed=seed, root_reward=np.zeros(B, np.float32),
+                        root_value=np.zeros(B, np.float32), root_policy=policy, root_beta=beta, root_noise=noises,
+                        noise_eps=0.0, reward=reward, value=value, policy=sim_policy, beta=sim_beta,
+                        meta=dict(deep_window=True, step=step))
+
+
 def run_search(tb, inp: SearchInputs, K: int, knobs: dict | None = None, record: bool = True,
                per_sim: bool = True):
     """Drive a Tree_batch-compatible object through one full search (mcts_sampled.py:89-191

@@ -94,10 +94,14 @@ class WeightBroadcaster:
     of the weights each rank now holds."""
 
     def __init__(self, model: torch.nn.Module, src: int = 0, group=None, checkpoint_interval: int = 1):
+        """`src` is the source's GLOBAL rank, as torch.distributed.broadcast takes it even with a
+        `group`; a group (e.g. the learner and the self-play ranks only) must contain it."""
         if checkpoint_interval < 1:
             raise ValueError("checkpoint_interval must be >= 1")
+        if group is not None and int(src) not in dist.get_process_group_ranks(group):
+            raise ValueError(f"source rank {src} is not in the broadcast group {dist.get_process_group_ranks(group)}")
         self.flat = FlatWeights(model)
-        self.src = src
+        self.src = int(src)
         self.group = group
         self.checkpoint_interval = int(checkpoint_interval)
         dev = next(iter(self.flat.flats.values())).device
@@ -116,7 +120,7 @@ class WeightBroadcaster:
         in place would have the source search newer weights than the other ranks until the next
         crossing, so publishing without a state_dict is refused there (index 0, the initial weights
         every rank pulls first, excepted)."""
-        if dist.get_rank(self.group) != self.src:
+        if dist.get_rank() != self.src:  # (global ranks on both sides: src is one)
             raise RuntimeError("only the source rank publishes weights")
         if state_dict is None and self.checkpoint_interval > 1 and int(model_index) > 0:
             raise ValueError("publish() needs the learner's state_dict when checkpoint_interval > 1 (the live "

@@ -34,7 +34,8 @@ sys.path.insert(0, ROOT)
 
 from mazero_amd import _capi  # noqa: E402
 from mazero_amd.cytree import Tree_batch  # noqa: E402
-from mazero_amd.synthetic import DEFAULTS, inputs_digest, make_search_inputs, run_search  # noqa: E402
+from mazero_amd.synthetic import (DEFAULTS, inputs_digest, make_deep_window_inputs, make_search_inputs,  # noqa: E402
+                                  run_search)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
@@ -62,6 +63,11 @@ CONFIGS = {
     # action spaces past one lane per action (round 5: expand_wide, k_hbm; refused before)
     "wide_a100_k5": (4, 100, 5, 40, 0.25, 0.3, False, {}),
     "wide_a255_k300": (2, 255, 300, 12, 0.25, 0.0, False, {}),
+    # one deep path per tree with a tie at its bottom (synthetic.make_deep_window_inputs, round 6):
+    # selections and next-expansion words past k_tree's 256-word LDS window of the engine stream;
+    # 383 nodes (k_tree<384>) and 603 (k_tree<1024>, the level walk)
+    "deep_window_k64_s190": (8, 2, 64, 190, 0.0, 0.0, "deep", {}),
+    "deep_window_k64_s300": (4, 2, 64, 300, 0.0, 0.0, "deep", {}),
 }
 
 
@@ -109,7 +115,10 @@ def record(lib, name, cfg, seed):
     knobs = dict(DEFAULTS)
     knobs.update(over)
     rng = np.random.default_rng(seed)
-    inp = make_search_inputs(rng, B, A, S, noise_eps=eps, legal_zero_frac=lz, ties=ties)
+    if ties == "deep":
+        inp = make_deep_window_inputs(rng, B, S, A)
+    else:
+        inp = make_search_inputs(rng, B, A, S, noise_eps=eps, legal_zero_frac=lz, ties=ties)
     tb = Tree_batch(B, 1, A, K, S, knobs["delta_lb"], inp.seed, knobs["rho"], knobs["lam"], lib=lib)
     out = run_search(tb, inp, K, knobs)
     arrays = dict(

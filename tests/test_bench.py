@@ -82,7 +82,9 @@ def test_gpus_flag_spawns_ranks(port_lib):
 
 def test_gpus_flag_eight_ranks(port_lib):
     """The driver's widest job, rehearsed on the CPU: `bench.py --gpus 8` over gloo with the port
-    backend, the metric's 256 roots split 32 per rank; rank 0 prints one line naming 8 ranks."""
+    backend, the metric's 256 roots split 32 per rank; rank 0 prints one line naming 8 ranks.  With
+    --broadcast-every 1 (BASELINE config #5's weight broadcast in the timed loop) the line carries
+    every rank's sync count, checkpoint and own time per sync."""
     import json
     import subprocess
 
@@ -90,7 +92,7 @@ def test_gpus_flag_eight_ranks(port_lib):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--backend", "port", "--sims", "4",
-           "--steps", "1", "--warmup", "1", "--no-cpu"]
+           "--steps", "2", "--warmup", "1", "--no-cpu", "--broadcast-every", "1"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -100,6 +102,14 @@ def test_gpus_flag_eight_ranks(port_lib):
     rk = line["ranks"]
     assert rk["world_size"] == 8 and [x["rank"] for x in rk["per_rank"]] == list(range(8))
     assert abs(max(x["ms_per_step"]["strong"] for x in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
+    # config #5's weight broadcast inside the timed loop (--broadcast-every 1): one sync per env step
+    # on every rank, each moving the 27m network's weights from rank 0 (warm-up sync + 2 timed)
+    wb = line["weight_broadcast"]
+    assert wb["every_steps"] == 1 and wb["syncs"] == 2 and wb["src_rank"] == 0 and wb["bytes"] > 1_000_000
+    assert wb["checkpoint"] == 3 and wb["transfers"] == 3 and "27m_vs_30m" in wb["network"]
+    assert len(wb["per_rank_ms_per_sync"]) == 8 and min(wb["per_rank_ms_per_sync"]) > 0
+    for x in rk["per_rank"]:
+        assert x["weight_broadcast"]["strong"]["syncs"] == 2 and x["weight_broadcast"]["strong"]["checkpoint"] == 3
 
 
 def test_strong_leg_is_the_global_batch(port_lib):

@@ -67,7 +67,22 @@ def test_product_library_builds_and_exports():
 
     lib = load()
     assert lib.mz_backend() == b"hip-gfx950"
-    assert lib.mz_abi_version() == 1
+    assert lib.mz_abi_version() == 2
+
+
+def test_abi_version_and_stat_table_match_header():
+    """MZ_ABI_VERSION, the enum mz_stat order and MZ_S_COUNT of include/mzmcts.h agree with the
+    binding's STATS table and the loader's ABI check (round 5 renumbered the stamp slots without a
+    version bump: ADVICE round 5)."""
+    from mazero_amd import _lib
+
+    txt = open(HEADER).read()
+    assert int(re.search(r"#define MZ_ABI_VERSION (\d+)", txt).group(1)) == _lib.ABI
+    enum = dict((k, int(v)) for k, v in re.findall(r"\b(MZ_S_[A-Z0-9_]+)\s*=\s*(\d+)", txt))
+    count = enum.pop("MZ_S_COUNT")
+    assert sorted(enum.values()) == list(range(count)) and len(_capi.STATS) == count
+    for name, v in enum.items():
+        assert _capi.STATS[v] == name[len("MZ_S_"):].lower(), name
 
 
 @pytest.mark.parametrize("path", [PORT_LIB, REF_LIB], ids=["port", "ref"])

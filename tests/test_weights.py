@@ -102,6 +102,71 @@ def test_gloo_two_ranks_broadcast():
     assert res == {0: [True] * 6, 1: [True] * 6}, res
 
 
+def _group_worker(rank, world, port, q):
+    """World size 4; the broadcast group is global ranks {1, 2, 3} (rank 0, e.g. a learner's peer,
+    left out) with the source at global rank 2, group rank 1: the source is named by its global
+    rank, as torch.distributed.broadcast takes it (publish compared a group rank
+    with it)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from mazero_amd.nets import make_net
+    from mazero_amd.weights import WeightBroadcaster
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group([1, 2, 3])  # (every rank takes part in new_group)
+    checks = []
+    try:
+        WeightBroadcaster(make_net(3, 9, seed=1), src=0, group=grp)
+        checks.append(False)
+    except ValueError:
+        checks.append(True)  # a source outside the group is refused
+    net = make_net(3, 9, seed=200 + rank)
+    if rank != 0:
+        wb = WeightBroadcaster(net, src=2, group=grp)
+        if rank == 2:
+            with torch.no_grad():
+                for p in net.parameters():
+                    p.add_(0.25)
+            wb.publish(5)
+        else:
+            try:
+                wb.publish(5)
+                checks.append(False)
+            except RuntimeError:
+                checks.append(True)  # only the source publishes
+        checks.append(wb.sync() == 5)
+    sd = {k: v.clone() for k, v in net.state_dict().items()}
+    ref = [None] * world
+    dist.all_gather_object(ref, sd)
+    key = next(iter(sd))
+    if rank != 0:
+        checks.append(all(torch.equal(ref[2][k], sd[k]) for k in sd))  # the source's weights arrived
+    else:
+        checks.append(not torch.equal(ref[2][key], sd[key]))  # rank 0 (outside the group) kept its own
+    q.put((rank, checks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_subgroup_broadcast_global_source_rank():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, 4, port, q)) for r in range(4)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(4))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: [True, True], 1: [True, True, True, True], 2: [True, True, True], 3: [True, True, True, True]}, res
+
+
 def _rccl_worker(port, q):
     import sys
 
