@@ -20,13 +20,15 @@ Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) every process i
 `python bench.py --gpus N` without torchrun starts the N ranks itself (torch.distributed.run, before
 anything touches the GPU) and n_gpus is the job's world size.  Roots are independent
 (cnode.cpp:633-641), so ranks share no data-path collective:
-  strong (headline, "scaling": "strong")  the metric's --roots (256) roots split over the ranks:
-         rank r searches rows [lo, hi) of the one global batch (global root offset lo, tree seeds
-         random_seed*2333 + global index), so the job is exactly BASELINE.json's 256 roots x 50 sims;
-  weak   (N > 1, reported beside it as "weak_scaling")  every rank searches its own --roots roots
-         (256*N roots in total, a bigger job than the metric names).
-`--weak` swaps the two (the metric string then names the 256*N roots).  The barrier /
-max-over-ranks clock uses torch.distributed (RCCL).
+  weak   (headline, "scaling": "weak")  every rank searches its own --roots (256) roots: the node's
+         self-play, one shard of environments per GPU as the reference runs one data worker per
+         GPU, each with its own 256-root searches; value = all ranks' simulations / the slowest
+         rank's time (the "whole node" of the metric);
+  strong (N > 1, reported beside it as "strong_scaling")  the --roots roots of ONE batch split over
+         the ranks: rank r searches rows [lo, hi) of the global batch (global root offset lo, tree
+         seeds random_seed*2333 + global index).  Bounded near 1.1x at 8 GPUs by the chain of
+         147 dependent launches per env step (profiles/round6/strong_proxy.json).
+`--strong` swaps the two.  The barrier / max-over-ranks clock uses torch.distributed (RCCL).
 
 Also reported (rank 0, N=1 only):
   roofline      dominant kernel = the fused simulation step (49 of 52 launches): algorithmic bytes per
@@ -71,11 +73,12 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--map", default="3m", choices=sorted(CONFIGS))
-    ap.add_argument("--roots", type=int, default=256, help="roots in total (strong scaling) / per GPU (weak)")
+    ap.add_argument("--roots", type=int, default=256, help="roots per GPU (weak scaling) / in total (strong)")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--sampled-times", type=int, default=1, help="K (core/config.py:86 default 1)")
-    ap.add_argument("--weak", action="store_true",
-                    help="headline value from the weak-scaling leg (--roots roots on every GPU)")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: headline value from the strong-scaling leg (--roots roots split over the GPUs) "
+                         "instead of the weak one (--roots roots on every GPU)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -653,12 +656,12 @@ def main():
         def make_leg(inputs, off):
             return PortLeg(args, inputs, off)
 
-    # strong scaling (headline): the --roots roots of one global batch split over the ranks, rank r
-    #   searching rows [lo, hi) of every agent search's inputs (global root offset lo)
-    # weak scaling: every rank owns --roots roots of its own (global root offset rank * roots)
+    # weak scaling (headline): every rank owns --roots roots of its own (global root offset rank * roots)
+    # strong scaling: the --roots roots of one global batch split over the ranks, rank r searching
+    #   rows [lo, hi) of every agent search's inputs (global root offset lo)
     # (one leg at world size 1, where the two are the same job)
     legs = {}
-    order = ["weak", "strong"] if args.weak else ["strong", "weak"]
+    order = ["strong", "weak"] if args.strong else ["weak", "strong"]
     if world == 1:
         order = order[:1]
     for kind in order:
@@ -718,11 +721,13 @@ def main():
                 roots_per_gpu=lg["B"],
                 steps=args.steps,
             )
-        if args.map == "3m" and args.roots == 256 and S == 50 and (main_kind == "strong" or world == 1):
+        if args.map == "3m" and args.roots == 256 and S == 50:
+            # (the per-search workload of BASELINE.json's metric on every GPU for the weak leg, split over
+            # the GPUs for the strong one; config.roots_total / roots_per_gpu say which)
             metric = "MCTS simulations/sec (whole node), SMAC 3m, 256 roots×50 sims, 1/2/4/8 GPUs"
         else:
-            metric = (f"MCTS simulations/sec (whole node), SMAC {args.map}, {m['total']} roots×{S} sims"
-                      + (f" ({m['B']} per GPU, weak scaling)" if main_kind == "weak" and world > 1 else ""))
+            metric = (f"MCTS simulations/sec (whole node), SMAC {args.map}, {args.roots} roots×{S} sims"
+                      + (" per GPU" if main_kind == "weak" and world > 1 else ""))
         if args.dropin:
             metric = (f"MCTS simulations/sec, tree-level drop-in (reference driver loop on mazero_amd.cytree, "
                       f"host numpy arrays), SMAC {args.map}, {m['total']} roots×{S} sims")
@@ -754,7 +759,9 @@ def main():
                 "graph": hip and not args.no_graph and not args.dropin,
                 "dropin": bool(args.dropin),
                 "backend": args.backend,
-                "parallelism": f"roots sharded over {world} GPU(s), no collective on the data path",
+                "parallelism": (f"{world} GPU(s), {m['B']} roots each, no collective on the data path"
+                                if main_kind == "weak" else
+                                f"{m['total']} roots sharded over {world} GPU(s), no collective on the data path"),
             },
             **other,
             **({"ranks": ranks} if ranks is not None else {}),

@@ -196,8 +196,8 @@ __host__ __device__ __forceinline__ void arena_nodes(Dev &d, unsigned B, unsigne
     d.o_hdr = d.o_C + s16;
 }
 // pUCT coefficient table entries, T[n (n + 1) / 2 + v] = pb_c(n, v) for n < PS, padded to 4.  Only
-// k_step's LDS-staged table (4 TT <= kTableLdsMax: PS <= 155) and the k_tree level-walk classes
-// (value entries E <= kBkCap: PS <= 342) read past T[0]; every other kernel computes pb_c from the
+// k_step's LDS-staged table (4 TT <= kTableLdsMax: PS <= 155) and k_tree's prior scores (value
+// entries E <= kBkCap: PS <= 342) read past T[0]; every other kernel computes pb_c from the
 // per-n pb / sq tables with the same double arithmetic.  Past kTableFullPS the table is T[0] alone,
 // O(S) instead of O(S^2) on host and device (S = 65,000 would need 8.5 GB).
 constexpr unsigned kTableFullPS = 512;
@@ -4049,7 +4049,7 @@ constexpr int kBkN = (NC <= 384) ? MZ_TREE_BK : (NC >= 1024 ? MZ_TREE_BK1024 : M
 template <int NC>
 constexpr int kTreeWavesN = kBkN<NC> + 1;
 constexpr int kBkCap = 340;  // value entries per staging slot (two per wave): S + 1 <= 340
-static_assert(kBkCap + 2 <= (int)kTableFullPS, "the k_tree level walk reads the full pUCT table");
+static_assert(kBkCap + 2 <= (int)kTableFullPS, "k_tree's prior scores read the full pUCT table");
 // the 512-node class with seven back-propagation waves keeps two workgroups per CU (76 KB of LDS
 // each) with slots of 128 entries (S + 1 <= 128; larger searches take k_step); so does kTree1024S
 template <int NC>

@@ -296,7 +296,8 @@ class _SearchLoop:
 # device arena (_TREES), each agent loop its captured graph (_LOOPS), and the loops of one geometry
 # share one hidden-state pool (_POOLS), so that a 27-agent self-play step holds one [S+1, B, N*H]
 # pool, not 27.  Every key carries the calling thread: two threads never share a handle (a handle is
-# single-threaded, include/mzmcts.h) or a pool.  Both caches are LRU-bounded (MZ_MAX_TREES,
+# single-threaded, include/mzmcts.h) or a pool; a pool's key also carries the stream its first loop
+# ran on.  Both caches are LRU-bounded (MZ_MAX_TREES,
 # MZ_MAX_LOOPS); release() empties them.
 _LOCK = threading.RLock()
 _LOOPS: "OrderedDict" = OrderedDict()
@@ -318,7 +319,10 @@ class _Pool:
 
 
 def _shared_pool(dev, S: int, B: int, cols: int, dtype) -> _Pool:
-    key = (threading.get_ident(), str(dev), S + 1, B, int(cols), dtype)
+    # (the current stream too: loops that a thread runs on different streams may overlap on the
+    # device, so they must not share a pool -- ADVICE round 5; loops on one stream run in order)
+    stream = torch.cuda.current_stream(dev).cuda_stream if torch.device(dev).type == "cuda" else 0
+    key = (threading.get_ident(), stream, str(dev), S + 1, B, int(cols), dtype)
     with _LOCK:
         p = _POOLS.get(key)
         if p is None:
@@ -376,6 +380,9 @@ def _storage_signature(model) -> tuple:
 # reference does (:89).
 
 
+MAX_GLUE_ACTIONS = 64  # include/mzdriver.h: the glue kernels hold one action per lane
+
+
 class SampledMCTS:
     """mcts_sampled.py:29-32.  `lib` selects the tree library (default: the MI355X product)."""
 
@@ -387,6 +394,13 @@ class SampledMCTS:
         the whole batch and sliced, and tree i is seeded with its global index, so a rank's results
         equal rows [lo, hi) of the unsharded search."""
         self.config = config
+        if int(config.action_space_size) > MAX_GLUE_ACTIONS:
+            # the device driver glue (mz_policy_glue, mz_root_glue, mz_joint_action: one lane per
+            # action) refuses wider action spaces; refused here, before any search launches (the
+            # drop-in Tree_batch surface itself takes A <= 255)
+            raise RuntimeError(f"SampledMCTS: action_space_size {config.action_space_size} > {MAX_GLUE_ACTIONS} "
+                               "(the device driver glue takes one lane per action; mazero_amd.cytree.Tree_batch "
+                               "takes up to 255)")
         self.np_random = np.random if np_random is None else np_random
         self._lib = lib
         if root_shard is not None:

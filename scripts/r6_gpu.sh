@@ -81,6 +81,13 @@ for st in $STEPS; do
         timeout -k 10 200 python bench.py --no-cpu --roots $r > $O/strong_$r.json 2> $O/strong.err || { tail -5 $O/strong.err; exit 1; }
         echo "roots $r: $(grep -o '"ms_per_step": [0-9.]*' $O/strong_$r.json | head -1) $(grep -o '"avg_launch_us": [0-9.]*' $O/strong_$r.json)"
       done ;;
+    bcast)
+      # config #5's weight broadcast in the timed loop (one rank: RCCL single-rank group)
+      timeout -k 10 300 python bench.py --no-cpu --broadcast-every ${BEVERY:-1} ${BARGS:-} > $O/bcast.json 2> $O/bcast.err \
+        || { tail -5 $O/bcast.err; exit 1; }; cat $O/bcast.json ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; rc=$?; tail -2 $O/smoke.log
+      [ $rc -ne 0 ] && exit $rc ;;
     bench)
       timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err; rc=$?; cat $O/bench.json; [ $rc -ne 0 ] && exit $rc ;;
   esac

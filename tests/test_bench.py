@@ -17,7 +17,7 @@ def test_defaults_are_the_headline_config():
 
     a = bench.parse([])
     assert (a.map, a.roots, a.sims, a.sampled_times) == ("3m", 256, 50, 1)
-    assert not a.weak and not a.no_graph
+    assert not a.strong and not a.no_graph and a.broadcast_every == 0
 
 
 def test_cpu_baseline_fields(port_lib):
@@ -37,10 +37,10 @@ def test_cpu_baseline_fields(port_lib):
 
 def test_gpus_flag_spawns_ranks(port_lib):
     """`bench.py --gpus 2` without torchrun starts two ranks itself (torch.distributed.run), each
-    rank reports the job's world size, and rank 0 prints one JSON line.  `value` is the strong leg:
-    the metric's --roots roots split over the ranks (BASELINE.json names 256 roots at 1/2/4/8 GPUs);
-    the weak leg (--roots per rank) rides beside it.  --backend port keeps it on the CPU (gloo): the
-    plumbing, not a measurement."""
+    rank reports the job's world size, and rank 0 prints one JSON line.  `value` is the weak leg:
+    every rank searches its own --roots roots (one shard of the node's self-play per GPU, the
+    "whole node" of the metric); the strong leg (--roots roots split over the ranks) rides beside
+    it.  --backend port keeps it on the CPU (gloo): the plumbing, not a measurement."""
     import json
     import subprocess
 
@@ -54,11 +54,11 @@ def test_gpus_flag_spawns_ranks(port_lib):
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
-    assert line["config"]["roots_total"] == 8 and line["config"]["roots_per_gpu"] == 4
-    assert "8 roots" in line["metric"] and "weak" not in line["metric"]
-    wk = line["weak_scaling"]
-    assert wk["roots_total"] == 16 and wk["roots_per_gpu"] == 8 and wk["value"] > 0
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["roots_total"] == 16 and line["config"]["roots_per_gpu"] == 8
+    assert "8 roots" in line["metric"] and "per GPU" in line["metric"]
+    st = line["strong_scaling"]
+    assert st["roots_total"] == 8 and st["roots_per_gpu"] == 4 and st["value"] > 0
     assert line["value"] > 0
     # the line verifies itself: the collective's world size, every rank's device and own step time
     # in both legs; the headline ms_per_step is the max over ranks
@@ -69,20 +69,21 @@ def test_gpus_flag_spawns_ranks(port_lib):
     for r in rk["per_rank"]:
         assert set(r["ms_per_step"]) == {"strong", "weak"} and min(r["ms_per_step"].values()) > 0
         assert r["device"] == "cpu"
-    assert abs(max(r["ms_per_step"]["strong"] for r in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
-    assert abs(max(r["ms_per_step"]["weak"] for r in rk["per_rank"]) - wk["ms_per_step"]) < 1e-3
-    # --weak: the weak leg is the headline, under a metric string that names its 16 roots
-    r = subprocess.run(base + ["--weak"], env=env, capture_output=True, text=True, timeout=300)
+    assert abs(max(r["ms_per_step"]["weak"] for r in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
+    assert abs(max(r["ms_per_step"]["strong"] for r in rk["per_rank"]) - st["ms_per_step"]) < 1e-3
+    # --strong: the strong leg is the headline (the 8 roots split over the two ranks)
+    r = subprocess.run(base + ["--strong"], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
-    assert line["scaling"] == "weak" and line["config"]["roots_total"] == 16
-    assert "16 roots" in line["metric"] and "weak scaling" in line["metric"]
-    assert line["strong_scaling"]["roots_total"] == 8
+    assert line["scaling"] == "strong" and line["config"]["roots_total"] == 8
+    assert "8 roots" in line["metric"] and "per GPU" not in line["metric"]
+    assert line["weak_scaling"]["roots_total"] == 16
 
 
 def test_gpus_flag_eight_ranks(port_lib):
     """The driver's widest job, rehearsed on the CPU: `bench.py --gpus 8` over gloo with the port
-    backend, the metric's 256 roots split 32 per rank; rank 0 prints one line naming 8 ranks.  With
+    backend, 256 roots on every rank (the strong leg beside it: 32 per rank); rank 0 prints one line
+    naming 8 ranks.  With
     --broadcast-every 1 (BASELINE config #5's weight broadcast in the timed loop) the line carries
     every rank's sync count, checkpoint and own time per sync."""
     import json
@@ -98,10 +99,13 @@ def test_gpus_flag_eight_ranks(port_lib):
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 8 and line["config"]["roots_total"] == 256 and line["config"]["roots_per_gpu"] == 32
+    assert line["n_gpus"] == 8 and line["scaling"] == "weak"
+    assert line["config"]["roots_total"] == 2048 and line["config"]["roots_per_gpu"] == 256
+    assert line["metric"].endswith("SMAC 3m, 256 roots×4 sims per GPU")
+    assert line["strong_scaling"]["roots_total"] == 256 and line["strong_scaling"]["roots_per_gpu"] == 32
     rk = line["ranks"]
     assert rk["world_size"] == 8 and [x["rank"] for x in rk["per_rank"]] == list(range(8))
-    assert abs(max(x["ms_per_step"]["strong"] for x in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
+    assert abs(max(x["ms_per_step"]["weak"] for x in rk["per_rank"]) - line["ms_per_step"]) < 1e-3
     # config #5's weight broadcast inside the timed loop (--broadcast-every 1): one sync per env step
     # on every rank, each moving the 27m network's weights from rank 0 (warm-up sync + 2 timed)
     wb = line["weight_broadcast"]
@@ -109,7 +113,8 @@ def test_gpus_flag_eight_ranks(port_lib):
     assert wb["checkpoint"] == 3 and wb["transfers"] == 3 and "27m_vs_30m" in wb["network"]
     assert len(wb["per_rank_ms_per_sync"]) == 8 and min(wb["per_rank_ms_per_sync"]) > 0
     for x in rk["per_rank"]:
-        assert x["weight_broadcast"]["strong"]["syncs"] == 2 and x["weight_broadcast"]["strong"]["checkpoint"] == 3
+        for kind in ("weak", "strong"):
+            assert x["weight_broadcast"][kind]["syncs"] == 2 and x["weight_broadcast"][kind]["checkpoint"] == 3
 
 
 def test_strong_leg_is_the_global_batch(port_lib):

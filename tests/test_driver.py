@@ -1029,3 +1029,15 @@ def test_root_glue_matches_host_root_inputs(dtype, A):
                                               err_msg=f"{name} {where}")
             np.testing.assert_array_equal(arrays["rewards"], rr)
             np.testing.assert_array_equal(arrays["values"], rv)
+
+
+def test_wide_action_space_refused_at_construction():
+    """the device driver glue takes one lane per action (A <= 64); SampledMCTS
+    refuses a wider action space in its constructor, before any search launches (CPU: no device
+    call is made), while the drop-in Tree_batch takes A <= 255."""
+    from mazero_amd.mcts_sampled import MAX_GLUE_ACTIONS, SampledMCTS
+    from mazero_amd.nets import SearchConfig
+
+    with pytest.raises(RuntimeError, match="action_space_size 65"):
+        SampledMCTS(SearchConfig(action_space_size=MAX_GLUE_ACTIONS + 1))
+    SampledMCTS(SearchConfig(action_space_size=MAX_GLUE_ACTIONS))

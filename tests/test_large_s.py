@@ -4,7 +4,7 @@ The reference computes pb_c = (logf((n + c2 + 1) / c2) + c1) * sqrt(n) / (v + 1)
 (cnode.cpp:313-316) and has no bound on simulation_num.  Until round 6 mz_create tabulated it for
 every (n, v) with n < S + 2, an O(S^2) table on host and device (8.5 GB at S = 65,000) whose size
 was computed in 32-bit ints (it wrapped past S = 32,767).  Now only the kernels that
-read the full table get one (k_step's LDS-staged table, the k_tree level-walk classes: S + 2 <= 342);
+read the full table get one (k_step's LDS-staged table, k_tree's prior scores: S + 2 <= 342);
 every other kernel computes pb_c from the per-n pb / sqrt tables with the same double arithmetic,
 and past 512 the table is T[0] alone (mazero_amd/csrc/mzmcts.hip `table_entries`).
 """
