@@ -4422,6 +4422,22 @@ constexpr bool kTreeW1Gather = false;
 constexpr bool kTreeW1Gather = !kTreeLevels<NC>;
 #endif
 
+// Round-6 experiment (-DMZ_SCORE_WALK): in the precomputed classes, after barrier (2) the four waves
+// score every node (S1) and each chase copy then walks from the root over those scores (score_walk:
+// per level the children's scores in one LDS round trip, the sequential arg-max in closed form by a
+// DPP row max and two ballots) instead of resolving every internal node's tie list (S2) and chasing
+// the resolved outcomes (tree_chase).  Bit-exact (the GPU suite passes on it), but slower: wave 0's
+// stamps at 3m K = 5 put S1 at ~1,400 cycles and S2 at ~1,380, and a walked level at ~950 cycles
+// against ~460 per chased level (its serial chain of LDS round trip, DPP max, readfirstlane, two
+// ballots and readlanes), so S1 + walk ~5,200 against S1 + S2 + chase ~4,600; fused launch
+// 7.26 -> 8.47 us, 3m K = 10 7.50 -> 8.13, 3s5z K = 5 10.10 -> 10.96 (profiles/round6/ab).
+template <int NC>
+#ifdef MZ_SCORE_WALK
+constexpr bool kTreeScoreWalk = !kTreeLevels<NC>;
+#else
+constexpr bool kTreeScoreWalk = false;
+#endif
+
 template <int NC>
 #ifdef MZ_C_W4
 constexpr bool kTreeCW4 = true;
@@ -4580,6 +4596,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
             if (vs < 0) vs = 0;
             if (vs > 1) vs = 1;
             sSc[n] = sSc[n] + vs;  // prior_score + value_score
+            if constexpr (kTreeScoreWalk<NC>) sQ[n] = i2f(vis);  // (score_walk: visits after the back-propagation)
         }
     }
     if (MZ_STAMPS && tp) {
@@ -4587,6 +4604,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
         tp[0] = __builtin_amdgcn_s_memtime();
     }
     lds_barrier();  // (3)
+    if constexpr (kTreeScoreWalk<NC>) return;  // (no tie lists: the walk resolves its own levels)
 #endif
     for (int p0 = wv * kWave; p0 < ntot; p0 += 4 * kWave) {  // (S2)
         const int p = p0 + l;
@@ -4790,6 +4808,113 @@ __device__ __forceinline__ void tree_chase(unsigned char *smem, const Dev &d, in
     }
     if (cursor > gW) err |= kErrRng;  // a consumed word beyond the stream
     if (Dn == 0) err |= kErrRoot;
+}
+
+// select_path (cnode.cpp:381-413) over the scores of tree_select_prep's S1 (sSc: every node's ucb_score
+// under its parent after this back-propagation; sQ: its visits).  The interface and outcomes of
+// tree_chase: per level one LDS round trip for the children's scores, structure records and visits
+// (lane j = child j), the first maximum by a DPP row max (a wave max past 16 children) and
+// select_child's tie list (cnode.cpp:355-370) in closed form, one engine word per non-empty list
+// (gen() % size, cnode.cpp:373-377), the next level's records from the chosen lane.
+template <int NC, bool REC>
+__device__ __forceinline__ void score_walk(unsigned char *smem, const Dev &d, int t, int gW, int wbase, int wsh,
+                                           int PS, int &cursor, int &err, int &Dn, int &x, int &xprev, int &px,
+                                           int &nbw) {
+    using L = TreeLayout<NC>;
+    const int l = lane_id();
+    const int4 *sA = (const int4 *)(smem + L::oA);
+    const int4 *sB = (const int4 *)(smem + L::oB);
+    const float *sSc = (const float *)(smem + L::oPS);
+    const int *sVis = (const int *)(smem + L::oQ);
+    int2 *sPath = (int2 *)(smem + L::oPath);
+    const unsigned *sRng = (const unsigned *)(smem + L::oRng);
+    cursor = uni(cursor);
+    int xv = uni(sA[0].x) + 1;  // the root is on every back-propagated path
+    int xb_x = uni(sB[0].x), xb_y = uni(sB[0].y);
+    x = 0;
+    while (true) {
+        const int nc = uni(nc_of(xb_y));
+        if (nc == 0) break;  // a leaf
+        const int fc = uni(xb_x);
+        const bool has = l < nc;
+        float sc = -INFINITY;
+        int cbx = 0, cby = 0, cvis = 0;
+        if (has) {
+            sc = sSc[fc + l];
+            const int2 cb = *(const int2 *)&sB[fc + l];
+            cbx = cb.x;
+            cby = cb.y;
+            cvis = sVis[fc + l];
+        }
+        int ci = 0;
+        if (x == 0 && xv <= nc) {
+            ci = xv - 1;  // forced root round-robin (cnode.cpp:398-399): no word
+        } else {
+            const int np = xv - 1;  // total_children_visit_counts = node->visit_count - 1
+            if (np < 0 || np >= PS) {
+                err |= kErrTable;
+                break;
+            }
+            float M;
+            if (nc <= 16) {  // one DPP row holds every child
+                float v = sc;
+                v = fmaxf(v, i2f(dpp<0xB1>(f2i(v))));
+                v = fmaxf(v, i2f(dpp<0x4E>(f2i(v))));
+                v = fmaxf(v, i2f(dpp<0x141>(f2i(v))));
+                v = fmaxf(v, i2f(dpp<0x140>(f2i(v))));
+                M = unif(v);
+            } else {
+                M = unif(wave_max(sc));
+            }
+            unsigned long long lst;
+            if (M > -1000000.0f) {  // FLOAT_MIN (utils.h:12)
+                const unsigned long long first = ballot(has && sc == M);
+                const int r = uni(__builtin_ctzll(first));
+                lst = ballot(has && sc >= M - 0.000001f) & (~0ull << r);
+            } else {
+                lst = ballot(has && sc >= -1000000.0f);
+            }
+            const int cnt = uni(__popcll(lst));
+            if (cnt > 0) {
+                if (cursor >= gW) {
+                    err |= kErrRng;
+                    break;
+                }
+                if (cnt > 1) {  // ties: the engine word modulo the list size picks the listed child
+                    const int o = cursor - wbase + wsh;
+                    const bool inwin = o >= wsh && o < kRngWin;
+                    if (!inwin) ++nbw;  // (MZ_S_RNG_TIE_BEYOND)
+                    const unsigned w = inwin ? (unsigned)uni((int)sRng[o]) : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                    for (int k = uni((int)(w % (unsigned)cnt)); k > 0; --k) lst &= lst - 1ull;
+                }
+                ++cursor;
+                ci = uni(__builtin_ctzll(lst));
+            }
+        }
+        if (Dn + 1 >= PS) {
+            err |= kErrPath;
+            break;
+        }
+        xprev = x;
+        x = uni(fc + ci);
+        ++Dn;
+        if (Dn < kWave) px = wl(px, x, Dn);
+        else if (REC && l == 0) sPath[Dn] = make_int2(x, 0);
+        xv = uni(rl(cvis, ci));
+        xb_x = uni(rl(cbx, ci));
+        xb_y = uni(rl(cby, ci));
+    }
+    if (Dn == 0) err |= kErrRoot;
+}
+
+// the precomputed classes' selection from the state tree_select_prep left: score_walk or tree_chase
+template <int NC, bool REC>
+__device__ __forceinline__ void tree_select(unsigned char *smem, const Dev &d, int t, int gW, int wbase, int wsh, int PS,
+                                            int &cursor, int &err, int &Dn, int &x, int &xprev, int &px, int &nbw) {
+    if constexpr (kTreeScoreWalk<NC>)
+        score_walk<NC, REC>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px, nbw);
+    else
+        tree_chase<NC, REC>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px, nbw);
 }
 
 template <int NC, bool SEL = true>  // SEL = false: the last expansion of a search (mz_expand_backup)
@@ -5012,7 +5137,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 const int gW2 = pl->g.W;
                 d.o_R = pl->d.o_R;
                 int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0, e = 0, nbw = 0;
-                tree_chase<NC, false>(smem, d, t, gW2, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px, nbw);
+                tree_select<NC, false>(smem, d, t, gW2, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px, nbw);
                 if (!e) {
                     TreeHdr *hp = d.hdr() + t;
                     const int wb = uni(xi[62]), ws = uni(xi[59]);
@@ -5131,7 +5256,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 // record {node, visits at selection} for the next back-propagation and the scored
                 // children's count (wave 0's epilogue leaves both to this wave)
                 int cur = uni(xi[58]), Dn = 0, x = 0, xprev = 0, px = 0, nbw = 0;
-                tree_chase<NC, true>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px, nbw);
+                tree_select<NC, true>(smem, d, t, gW1, uni(xi[62]), uni(xi[59]), PS, cur, e, Dn, x, xprev, px, nbw);
                 auto write_path = [&]() {
                     int2 *gp = d.path() + (size_t)t * PS;
                     const int2 *sPath1 = (const int2 *)(smem + L::oPath);
@@ -5605,7 +5730,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         stamp(ts, 5);
     if (!err) {
         int xprev = 0;
-        tree_chase<NC, true>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px, nbeyond);
+        tree_select<NC, true>(smem, d, t, gW, wbase, wsh, PS, cursor, err, Dn, x, xprev, px, nbeyond);
         out_idx = uni(sB[Dn == 0 ? 0 : xprev].w);  // parent->hidden_state_index_x
         out_act = act_of(uni(sB[x].y));            // children_action of the last edge
     }
@@ -5760,6 +5885,25 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         add = sel_lane(add, (long long)moved, 1ull << MZ_S_MM_MOVED);
         add = sel_lane(add, (long long)nbeyond, 1ull << MZ_S_RNG_TIE_BEYOND);
         add = sel_lane(add, (long long)nxbeyond, 1ull << MZ_S_RNG_NXT_BEYOND);
+#ifdef MZ_STAMPS_W0
+        // (diagnostic builds with -DMZ_STAMPS_W0: wave 0's eight phases in slots CYC_HEADER + k = ts[k+1]
+        // - ts[k]: round 1, barrier (1), expansion, barrier (2), scores + tie lists (precomputed
+        // classes; 0 in the level walk), chase / walk, path record, epilogue)
+        if (MZ_STAMPS && l >= MZ_S_CYC_HEADER && l < MZ_S_CYC_HEADER + 8) {
+            const int k = l - MZ_S_CYC_HEADER;
+            unsigned long long d0 = 0, d1 = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q == k) {
+                    d0 = ts[q];
+                    d1 = ts[q + 1];
+                }
+            add = (long long)(d1 - d0);
+        } else if (MZ_STAMPS && l == MZ_S_STAMPED) {
+            add = 1;
+        }
+        if (false)
+#endif
         if (MZ_STAMPS) switch (l) {
             case MZ_S_CYC_HEADER: add = (long long)(ts[1] - ts[0]); break;    // round 1
             case MZ_S_CYC_STAGE2: add = (long long)(ts[2] - ts[1]); break;    // barrier (1) wait

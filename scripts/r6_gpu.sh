@@ -69,6 +69,19 @@ for st in $STEPS; do
       echo "graph pmc pass rc=$?"
       head -5 $O/segv_graph.txt 2>/dev/null
       exit 0 ;;
+    w0stamps)
+      # wave 0's eight k_tree phases (variant builds with -DMZ_STAMPS=1 -DMZ_STAMPS_W0): cfg:variant pairs
+      for pair in ${W0PAIRS:-3m_k5:w0prod 3m_k5:w0lev256}; do
+        cfg=${pair%%:*}; v=${pair##*:}
+        case $cfg in
+          3m_k5) a="--sampled-times 5";; 3m_k10) a="--sampled-times 10";;
+          3s5z_k5) a="--map 3s5z_vs_3s6z --roots 512 --sims 100 --sampled-times 5";;
+          27m_k5) a="--map 27m_vs_30m --roots 256 --sims 200 --sampled-times 5";;
+        esac
+        MZ_STAMPS=1 MZ_LIB_OVERRIDE=$PWD/mazero_amd/_build/variant_$v.so timeout -k 10 200 python bench.py --no-cpu --steps 3 \
+          --warmup 1 $a > $O/w0_${cfg}_$v.json 2> $O/w0.err || { tail -5 $O/w0.err; exit 1; }
+        python -c "import json,sys; r=json.load(open('$O/w0_${cfg}_$v.json'))['roofline']; print('$cfg $v', r['avg_launch_us'], r.get('phase_cycles'))"
+      done ;;
     mut)
       # the beyond-window test against a build whose wave 1 chases without the stream offset (the
       # round-5 bug, mazero_amd/_build/variant_mut_w1_oR.so): expected to FAIL; never ends the pass
