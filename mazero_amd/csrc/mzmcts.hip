@@ -3660,7 +3660,13 @@ __global__ __launch_bounds__(192) void k_chain3(char *base, const float *policy,
                 sXl[2] = (long long)(ts[1] - ts[0]);                         // round 1
             }
         }
-        lds_barrier();
+        // no barrier: this wave's LDS writes are done when it ends, and a wave that has ended no longer
+        // counts at s_barrier, so wave 0's barrier (the exact case, the fused readback) completes once
+        // this wave has ended.  (With a barrier here this wave sat in it until wave 0 ended -- in the
+        // fast case wave 0 takes none -- and the MZ_SPANS build recorded it as the launch's last wave,
+        // 0.17 us after wave 0; without it the spans period is 3.20 -> 2.98 us, but the product's
+        // launch is unchanged, 3.10 us: wave 0 ends last either way, profiles/round6/ab)
+        wait_lds();
         span_end(hsx, 1);
         return;
     }
