@@ -4060,6 +4060,11 @@ static_assert(kBkCap + 2 <= (int)kTableFullPS, "k_tree's prior scores read the f
 // each) with slots of 128 entries (S + 1 <= 128; larger searches take k_step); so does kTree1024S
 template <int NC>
 constexpr int kBkCapN = (NC == kTree1024S || (NC == 512 && kBkN<NC> > 4)) ? 128 : kBkCap;
+// a staging slot's stride in int2 entries: CAP entries plus one of lead-in for the 16-byte DMA from
+// the aligned address below a node's first entry (its entries are 8-byte aligned), and one of
+// tail-out, an even count so that every slot starts 16-byte aligned
+template <int CAP>
+constexpr int kBkSlot = CAP + 2;
 // The 1024-node classes walk level by level instead (O(depth) after the barrier instead of
 // O(pool) / 4 waves).  Measured on one box, k_tree fused launch: 27m K = 5 (1010 nodes) 13.8 us by
 // levels against 14.1 us with tree_select_prep; 3m K = 5 (260 nodes) 10.4 against 11.6 us,
@@ -4107,7 +4112,7 @@ struct TreeLayout {
     static constexpr int CAP = kBkCapN<NC>;
     // staging int2s: two slots per back-propagation wave, at least 16 KiB for big leaf rows except in
     // kTree1024S (its rows up to 8 * kTreeReg bytes are staged, larger ones copied directly)
-    static constexpr int kTreeReg = (NC == kTree1024S || 2 * BK * CAP > kRegCap) ? 2 * BK * CAP : kRegCap;
+    static constexpr int kTreeReg = (NC == kTree1024S || 2 * BK * kBkSlot<CAP> > kRegCap) ? 2 * BK * kBkSlot<CAP> : kRegCap;
     // path levels: PS = S + 2 <= P / K <= NC / 2, and S + 1 <= CAP (the handle takes k_tree only then)
     static constexpr int PSx = (NC / 2 + 1 < CAP + 1) ? NC / 2 + 1 : CAP + 1;
     static constexpr int oA = 0;                                   // int4 [NC] staged {visit, prior, value, reward}
@@ -4172,6 +4177,7 @@ struct BkPre {
     int n0, nv0, n1, nv1;  // the pre-staged levels' nodes and entry counts (nv < 0: not staged)
     int ndma;              // LDS-DMA instructions issued for them (the wave's last ones before barrier (1))
     float4 c0, c1;         // their value-set scalars (scalar loads; unless kTreeCStage)
+    int sh0, sh1;          // their first entry's place in the slot (int2 units: 16-byte DMA from below it)
 };
 
 // The back-propagation's arena offsets as values of this point of the wave (they depend only on
@@ -4220,7 +4226,7 @@ template <int BK, int CAP>
 __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, int D, int k, int2 p0, int2 p1,
                                              int2 *sReg) {
     const int l = lane_id();
-    BkPre r{0, -1, 0, -1, 0, make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    BkPre r{0, -1, 0, -1, 0, make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f), 0, 0};
     const int2 *gV = d.V() + (size_t)t * P * E;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -4228,11 +4234,18 @@ __device__ __forceinline__ BkPre bk_prestage(const Dev &d, int t, int P, int E, 
         const int2 pe = j == 0 ? p0 : p1;
         if (i > D) break;
         if (pe.x < 0 || pe.x >= P || pe.y < 0 || pe.y > CAP) continue;  // (staged after barrier (1))
-        const int *src = (const int *)(gV + (size_t)pe.x * E);
-        int *dst = (int *)(sReg + (2 * k + j) * CAP);
-        for (int c = 0; c < 2 * pe.y; c += kWave)
-            if (c + l < 2 * pe.y) glds4a(src + c + l, dst + c);
-        r.ndma += (2 * pe.y + kWave - 1) / kWave;
+        // 16-byte LDS-DMA from the aligned address at or below the node's first entry (four times the
+        // bytes per instruction of 4-byte chunks; the chunks past the last entry read the next node's)
+        const int2 *src = gV + (size_t)pe.x * E;
+        const int sh = (int)(((uintptr_t)src >> 3) & 1);  // 8 bytes past a 16-byte boundary
+        const int4 *asrc = (const int4 *)(src - sh);
+        int2 *dst = sReg + (2 * k + j) * kBkSlot<CAP>;
+        const int n16 = (sh + pe.y + 1) >> 1;
+        for (int c = 0; c < n16; c += kWave)
+            if (c + l < n16) glds16a(asrc + c + l, (int4 *)dst + c);
+        r.ndma += (n16 + kWave - 1) / kWave;
+        if (j == 0) r.sh0 = sh;
+        else r.sh1 = sh;
         // (scalar loads, counted by lgkmcnt: landed by the first LDS wait after barrier (1))
         const float4 cw = (kTreeCStage) ? make_float4(0.f, 0.f, 0.f, 0.f) : ldsc4(d.C() + (size_t)t * P + pe.x);
         if (j == 0) {
@@ -4314,11 +4327,11 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         const float key = boot[i];
         const int2 *R;
         if (j == 0 && pre.nv0 >= 0) {
-            R = sReg + (2 * k) * CAP;
+            R = sReg + (2 * k) * kBkSlot<CAP> + pre.sh0;
         } else if (j == 1 && pre.nv1 >= 0) {
-            R = sReg + (2 * k + 1) * CAP;
+            R = sReg + (2 * k + 1) * kBkSlot<CAP> + pre.sh1;
         } else {  // a later level (or a pre-stage that did not match): slot 0, free once level j - 2 is done
-            int2 *dst = sReg + (2 * k) * CAP;
+            int2 *dst = sReg + (2 * k) * kBkSlot<CAP>;
             const int *src = (const int *)(gV + (size_t)n * g.E);
             for (int c = 0; c < 2 * nv; c += kWave)
                 if (c + l < 2 * nv) glds4a(src + c + l, (int *)dst + c);
@@ -4329,22 +4342,30 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         // entries of a smaller depth / the same depth / the same depth and a smaller value; none but
         // smaller depths when the node's deepest entry is above dep (stage_regions' need test)
         int lo = nv, c = 0, pv = 0;
+        // (a node of at most one wave of entries keeps them in lane e's registers: the order
+        // statistic and the tail shift below then read no LDS)
+        const bool reg1 = nv <= kWave;
+        int2 e1 = make_int2(0x7fffffff, 0);
         if (nv > 0 && md_of(by) >= dep) {
             lo = 0;
             for (int e0 = 0; e0 < nv; e0 += kWave) {
                 const bool on = e0 + l < nv;
                 const int2 e = on ? R[e0 + l] : make_int2(0x7fffffff, 0);
+                if (e0 == 0) e1 = e;
                 lo += __popcll(ballot(on && e.x < dep));
                 c += __popcll(ballot(on && e.x == dep));
                 pv += __popcll(ballot(on && e.x == dep && i2f(e.y) < key));
             }
             ent_r += nv;
         }
+        auto entry_y = [&](int i) {  // R[i].y, 0 <= i < nv, read only after the pass above loaded R
+            return reg1 ? rl(e1.y, i) : R[i].y;
+        };
         float ws = cw.x, tw = cw.y;
         const int cur = (c == 0) ? 0 : value_lim(c, g.one_minus_rho);
         const int nl = value_lim(c + 1, g.one_minus_rho);
         if (cur == nl) {  // SubTreeValueSet::update (utils.cpp:20-71)
-            const float mb = i2f(R[lo + c - cur].y);  // *big.begin()
+            const float mb = i2f(entry_y(lo + c - cur));  // *big.begin()
             if (!(key < mb)) {
                 ws -= lp * mb;
                 tw -= lp;
@@ -4357,7 +4378,7 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
                 tw += lp;
                 ws += lp * key;
             } else {
-                const float ms = i2f(R[lo + c - cur - 1].y);  // *(--small.end())
+                const float ms = i2f(entry_y(lo + c - cur - 1));  // *(--small.end())
                 if (key > ms) {
                     tw += lp;
                     ws += lp * key;
@@ -4375,8 +4396,12 @@ __device__ __forceinline__ void bk_levels(const Geo &g, const Dev &d, const Lds 
         } else if (l == 0) {
             G[pos] = make_int2(dep, f2i(key));
         }
-        for (int e0 = pos; e0 < nv; e0 += kWave)  // the entries after the insertion point move up by one
-            if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
+        if (reg1) {  // the entries after the insertion point move up by one (from the registers)
+            if (l >= pos && l < nv) G[l + 1] = e1;
+        } else {
+            for (int e0 = pos; e0 < nv; e0 += kWave)
+                if (e0 + l < nv) G[e0 + l + 1] = R[e0 + l];
+        }
         ent_w += nv - pos + 1;
         const bool is_leaf = (i == D);  // its structure record belongs to the expanding wave
         int4 a4 = a4r;
@@ -4426,6 +4451,31 @@ template <int NC>
 constexpr bool kTreeW1Gather = false;
 #else
 constexpr bool kTreeW1Gather = !kTreeLevels<NC>;
+#endif
+
+// The waves that score every node and resolve the tie lists after barrier (2) (tree_select_prep):
+// four where a pass of four waves covers the pool (<= 256 nodes), every wave of the workgroup in the
+// larger classes, where four waves took two passes of each phase (round 6, same-box A/B against the
+// same build with four, MZ_SEL_W4: 3s5z K = 5 10.08 -> 9.98 us, 3m K = 10 unchanged at 7.60)
+template <int NC>
+#ifdef MZ_SEL_W4
+constexpr int kSelW = 4;
+#else
+constexpr int kSelW = (NC > 256 && !kTreeLevels<NC>) ? kTreeWavesN<NC> : 4;
+#endif
+
+// Round-6 experiment (-DMZ_HELPER_CDF): the leaf's sampling distribution (discrete_distribution's
+// probabilities and prefix sums, cnode.cpp:243-262) computed before barrier (1) by the last
+// back-propagation role (hardware wave 4, on wave 0's SIMD; its path levels are the deepest and
+// usually absent) while wave 0 waits for its round-1 loads, wave 0 reading the CDF after barrier (1).
+// Bit-exact, but slower in every configuration (same-box A/B against the same build without it:
+// 3m K = 5 7.22 -> 7.57 us, 3m K = 10 7.44 -> 7.60, 3s5z K = 5 9.92 -> 9.98, 27m K = 5
+// 11.43 -> 11.58; profiles/round6/ab): the helper's beta load and distribution delay barrier (1)
+// for every wave, and the expansion it shortens ends before the back-propagation anyway
+#ifdef MZ_HELPER_CDF
+constexpr bool kTreeHelperCdf = true;
+#else
+constexpr bool kTreeHelperCdf = false;
 #endif
 
 // Round-6 experiment (-DMZ_SCORE_WALK): in the precomputed classes, after barrier (2) the four waves
@@ -4588,7 +4638,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
 #else
     float2 *sRec = sAz;
     auto score = [&](int c) { return sSc[c]; };
-    for (int n0 = wv * kWave; n0 < ntot; n0 += 4 * kWave) {  // (S1)
+    for (int n0 = wv * kWave; n0 < ntot; n0 += kSelW<NC> * kWave) {  // (S1)
         const int n = n0 + l;
         if (n >= 1 && n < ntot) {
             const int4 a = sA[n];
@@ -4612,7 +4662,7 @@ __device__ __forceinline__ void tree_select_prep(unsigned char *smem, int wv, in
     lds_barrier();  // (3)
     if constexpr (kTreeScoreWalk<NC>) return;  // (no tie lists: the walk resolves its own levels)
 #endif
-    for (int p0 = wv * kWave; p0 < ntot; p0 += 4 * kWave) {  // (S2)
+    for (int p0 = wv * kWave; p0 < ntot; p0 += kSelW<NC> * kWave) {  // (S2)
         const int p = p0 + l;
         if (p < ntot) {
             const int4 b = sB[p];
@@ -4991,6 +5041,10 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         // ======== waves 2 .. kBk: stage the node records (waves 2, 3); back-propagate their path
         // levels; then the prior scores after the back-propagation and the min/max over the visited
         // nodes off the path ========
+        // (the helper role: the leaf's beta, one action per lane, first)
+        const bool cdf_helper = kTreeHelperCdf && wv == BK && A >= 2;
+        float hbet = 0.f;
+        if (cdf_helper && l < A) hbet = beta[(size_t)t * A + l];
         int2 bp0, bp1;
         bk_path_records<BK>(d, t, PS, wv - 1, bp0, bp1);
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
@@ -5047,6 +5101,13 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         // this wave's path levels' value entries: issued last, in flight across barrier (1)
         const BkPre pre = bk_prestage<BK, kBkCapN<NC>>(d, t, P, g.E, D, wv - 1, bp0, bp1, (int2 *)(smem + L::oReg));
         wait_vm_but(pre.ndma);
+        if (cdf_helper) {
+            // the leaf's CDF for wave 0's draws: cp[a] in oU (oIx: the weights' broadcast scratch, free
+            // until the epilogue)
+            double *hcp = (double *)(smem + L::oU);
+            const double cp = cdf_bcast(hbet, A, (float *)(smem + L::oIx), hcp);
+            hcp[l] = cp;  // (after this wave's own reads of the probabilities there)
+        }
         stamp(ts, 1);
         lds_barrier();  // (1)
         stamp(ts, 2);
@@ -5133,7 +5194,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         if (l == 0) xl[1 + wv] = (long long)span_mark();  // (diagnostic: arrival at barrier (2))
 #endif
         lds_barrier();  // (2)
-        if (SEL && !kTreeLevels<NC> && wv < 4) {
+        if (SEL && !kTreeLevels<NC> && wv < kSelW<NC>) {
             const int ncl = uni(xi[15]), err = bk_err<NC>(smem) | uni(xi[14]);
             tree_select_prep<NC>(smem, wv, err ? tot : tot + ncl, discount, gdel, PS, D);
             if (wv == 2 && !err) {  // (every fused launch of the precomputed classes: see wave 0's header)
@@ -5476,7 +5537,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     } else {
         double *sp = (double *)(smem + L::oP);
         wait_lds();
-        const double cp = cdf_staged(A, sW, sp);
+        const double cp = kTreeHelperCdf ? ((const double *)(smem + L::oU))[l] : cdf_staged(A, sW, sp);
         if (MZ_STAMPS) {
             asm volatile("" ::"v"(cp));
             stamp(tq, 1);
