@@ -4173,6 +4173,70 @@ static_assert(TreeLayout<kTree1024S>::total <= 80 * 1024, "kTree1024S: two workg
 // and launch, round 3).  MZ_C_STAGE builds the staged variant for A/B runs.
 // (kTreeCStage: defined with the class traits above)
 
+// Round-1 staging of k_tree's node records through registers instead of LDS-DMA (-DMZ_STAGE_VGPR,
+// round-6 experiment): every 16-byte record of two arrays loaded into VGPRs (all loads of a batch
+// issued together), then written to LDS.  Bit-exact; same-box A/B: 3m K = 5 7.27 -> 7.37 us, 3m
+// K = 10 7.44 -> 7.59, 3s5z K = 5 9.99 -> 9.91, 27m K = 5 11.48 -> 11.43 (profiles/round6/ab)
+#ifdef MZ_STAGE_VGPR
+constexpr bool kStageVgpr = true;
+#else
+constexpr bool kStageVgpr = false;
+#endif
+template <int MAXC>
+__device__ __forceinline__ void stage_regs16x2(const int4 *s0, int4 *d0, const int4 *s1, int4 *d1, int n) {
+    typedef int int4x __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) int4x gi4;
+    const int l = lane_id();
+    for (int b0 = 0; b0 < n; b0 += MAXC * kWave) {
+        int4x v0[MAXC], v1[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int i = b0 + c * kWave + l;
+            if (i < n) {
+                v0[c] = *((gi4 *)(const void *)s0 + i);
+                v1[c] = *((gi4 *)(const void *)s1 + i);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int i = b0 + c * kWave + l;
+            if (i < n) {
+                *((int4x *)(void *)d0 + i) = v0[c];
+                *((int4x *)(void *)d1 + i) = v1[c];
+            }
+        }
+    }
+}
+template <int MAXC>
+__device__ __forceinline__ void stage_regs4x3(const float *s0, float *d0, const float *s1, float *d1, const int *s2,
+                                              int *d2, int n) {
+    typedef const __attribute__((address_space(1))) float gf;
+    typedef const __attribute__((address_space(1))) int gi;
+    const int l = lane_id();
+    for (int b0 = 0; b0 < n; b0 += MAXC * kWave) {
+        float v0[MAXC], v1[MAXC];
+        int v2[MAXC];
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int i = b0 + c * kWave + l;
+            if (i < n) {
+                v0[c] = *((gf *)(const void *)s0 + i);
+                v1[c] = *((gf *)(const void *)s1 + i);
+                v2[c] = *((gi *)(const void *)s2 + i);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) {
+            const int i = b0 + c * kWave + l;
+            if (i < n) {
+                d0[i] = v0[c];
+                d1[i] = v1[c];
+                d2[i] = v2[c];
+            }
+        }
+    }
+}
+
 struct BkPre {
     int n0, nv0, n1, nv1;  // the pre-staged levels' nodes and entry counts (nv < 0: not staged)
     int ndma;              // LDS-DMA instructions issued for them (the wave's last ones before barrier (1))
@@ -5050,7 +5114,11 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         const float omr = pl->g.one_minus_rho, gdel = pl->g.delta;  // (issued with the header's loads)
         if constexpr (!kTreeLevels<NC>) bk_pin_offsets(d);  // (the 1024-node class: measured slower)
         const bool al = (P & 3) == 0;  // the tree's 4-byte arrays start 16-byte aligned
-        if (wv == 2) {
+        if (kStageVgpr && wv == 2) {
+            stage_regs16x2<(NC >= 512 ? 4 : NC / kWave)>(d.A() + nb, sA, d.Bn() + nb, sB, ne);
+        } else if (kStageVgpr && wv == 3) {
+            stage_regs4x3<(NC >= 512 ? 8 : NC / kWave)>(d.PP() + nb, sPP, d.Q() + nb, sQ, d.Par() + nb, sPar, ne);
+        } else if (wv == 2) {
             dma_dwords(d.A() + nb, lds_addr(smem) + L::oA, 4 * ne, true);
             dma_dwords(d.Bn() + nb, lds_addr(smem) + L::oB, 4 * ne, true);
         } else if (wv == 3) {
