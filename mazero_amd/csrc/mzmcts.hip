@@ -5096,6 +5096,9 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
     BkOut *xbo = (BkOut *)(smem + L::oXB);
     const size_t nb = (size_t)t * P;
     unsigned long long ts[10] = {0};
+#ifdef MZ_STAMPS_WALK
+    unsigned long long tw[9] = {0};
+#endif
     stamp(ts, 0);
     const unsigned long long rt0 = span_open();
     const cTreeHdr *hp0 = (const cTreeHdr *)(d.hdr() + t);
@@ -5742,6 +5745,22 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         stamp(ts, 5);
     } else if constexpr (kTreeLevels<NC>) {
         stamp(ts, 5);
+#ifdef MZ_STAMPS_WALK
+        // (diagnostic builds with -DMZ_STAMPS_WALK -DMZ_STAMPS_W0: wave 0's slots become the walk's
+        // root reads, its passes 1..5 (0 past the last), and the exit)
+        tw[0] = __builtin_amdgcn_s_memtime();
+        int twn = 0;
+#define MZ_WALK_TOP()                                                          \
+    do {                                                                        \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();             \
+        if (twn == 0) tw[1] = n_; else if (twn == 1) tw[2] = n_;                \
+        else if (twn == 2) tw[3] = n_; else if (twn == 3) tw[4] = n_;           \
+        else if (twn == 4) tw[5] = n_; else if (twn == 5) tw[6] = n_;           \
+        ++twn;                                                                  \
+    } while (0)
+#else
+#define MZ_WALK_TOP() do {} while (0)
+#endif
     if (!err) {
         cursor = uni(cursor);
         const bool mm_on = mm_cnt > 0;
@@ -5755,12 +5774,134 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         int par_hsx = xb.w;
         pvv = wl(pvv, xv, 0);
         while (true) {
+            MZ_WALK_TOP();
             x = uni(x);
             xv = uni(xv);
             cursor = uni(cursor);
             const int nc = uni(nc_of(xb.y));
             if (nc == 0) break;
             const int fc = uni(xb.x);
+#ifndef MZ_NO_WALK2
+            if (nc <= 7) {
+                // Two levels per pass (nc <= 7 and every child's nc <= 8): lanes 0..7 hold x's children,
+                // lanes 8 + 8g + i child g's child i.  Each lane scores its node as the one-level pass
+                // below would at that node's level (the scores depend on the node and the launch's
+                // min-max only); one segmented DPP max over eight lanes gives every group's maximum, and
+                // the tie lists of all groups come from two ballots.  The first level's outcome picks
+                // the group whose list resolves the second; the engine words are consumed in the same
+                // order (one per scored level).  Bit-exact with two one-level passes.
+                const int g = (l >> 3) - 1;  // -1: x's children
+                const int sl = l & 7;
+                const bool lo = l < 8;
+                const bool has1 = (lo ? sl : g) < nc;
+                int4 ca = make_int4(0, 0, 0, 0), cb = ca;
+                float cpp = 0.f, cps = 0.f;
+                float2 caz = make_float2(0.f, 0.f);
+                int cfl = 0;
+                const float2 az1 = kTreeAzLevel<NC> ? sAz[Dn + 1] : make_float2(0.f, 0.f);
+                const float2 az2 = kTreeAzLevel<NC> ? sAz[Dn + 2] : make_float2(0.f, 0.f);  // Dn + 2 <= PS
+                if (has1) {
+                    const int n1 = fc + (lo ? sl : g);
+                    cb = sB[n1];  // (the groups: their parent's structure record)
+                    if (lo) {
+                        ca = sA[n1];
+                        cpp = sPP[n1];
+                        cps = sPS[n1];
+                        cfl = sFl[n1];
+                        if constexpr (!kTreeAzLevel<NC>) caz = sAz[n1];
+                    }
+                }
+                const int gnc = nc_of(cb.y);
+                const bool ok2 = ballot(!lo && has1 && gnc > 8) == 0ull;
+                const bool has2 = !lo && has1 && sl < gnc;
+                if (has2) {
+                    const int n2 = cb.x + sl;
+                    ca = sA[n2];
+                    cb = sB[n2];
+                    cpp = sPP[n2];
+                    cps = sPS[n2];
+                    cfl = sFl[n2];
+                    if constexpr (!kTreeAzLevel<NC>) caz = sAz[n2];
+                }
+                if constexpr (kTreeAzLevel<NC>) caz = lo ? az1 : az2;
+                const bool has = lo ? has1 : has2;
+                const int cvis = ca.x + (cfl ? 1 : 0);
+                float sc = -INFINITY;
+                if (has) {  // ucb_score (cnode.cpp:297-335), as below
+                    const float val = cfl ? caz.x : i2f(ca.z);
+                    const float rw = cfl ? caz.y : i2f(ca.w);
+                    float vs = (cvis == 0) ? 0.0f : ((rw + discount * val) - cpp);
+                    if (mm_on) vs = (vs - mmn) / den;
+                    if (vs < 0) vs = 0;
+                    if (vs > 1) vs = 1;
+                    sc = cps + vs;
+                }
+                float Ms = sc;  // the maximum of the lane's group of eight
+                Ms = fmaxf(Ms, i2f(dpp<0xB1>(f2i(Ms))));
+                Ms = fmaxf(Ms, i2f(dpp<0x4E>(f2i(Ms))));
+                Ms = fmaxf(Ms, i2f(dpp<0x141>(f2i(Ms))));
+                const bool big = Ms > -1000000.0f;
+                const unsigned long long bE = ballot(has && sc == Ms);
+                const float thr = big ? Ms - 0.000001f : -1000000.0f;
+                const unsigned long long bT = ballot(has && sc >= thr);
+                // one level's select_child from group `base`'s lanes: -1 (err set) ends the walk
+                auto pick = [&](int base, int ncl) -> int {
+                    if (x == 0 && xv <= ncl) return xv - 1;  // forced root round-robin (cnode.cpp:398-399)
+                    const int np = xv - 1;
+                    if (np < 0 || np >= PS) {
+                        err |= kErrTable;
+                        return -1;
+                    }
+                    nscored += ncl;
+                    unsigned long long lst = (bT >> base) & 0xffull;
+                    if (i2f(rl(f2i(Ms), base)) > -1000000.0f)
+                        lst &= ~0ull << uni(__builtin_ctzll((bE >> base) & 0xffull));
+                    const int cntl = uni(__popcll(lst));
+                    if (cntl == 0) return 0;
+                    if (cursor >= gW) {
+                        err |= kErrRng;
+                        return -1;
+                    }
+                    if (cntl > 1) {
+                        const int o = cursor - wbase + wsh;
+                        if (!(o >= wsh && o < kRngWin)) ++nbeyond;
+                        const unsigned w = (o >= wsh && o < kRngWin) ? (unsigned)uni((int)sRng[o])
+                                                                   : (unsigned)uni((int)d.R()[(size_t)t * gW + cursor]);
+                        for (int k = uni((int)(w % (unsigned)cntl)); k > 0; --k) lst &= lst - 1ull;
+                    }
+                    ++cursor;
+                    return uni(__builtin_ctzll(lst));
+                };
+                auto advance = [&](int fcl, int ln) -> bool {  // to the child in lane ln
+                    if (Dn + 1 >= PS) {
+                        err |= kErrPath;
+                        return false;
+                    }
+                    par_hsx = uni(xb.w);
+                    x = uni(fcl + (ln & 7));
+                    ++Dn;
+                    xv = uni(rl(cvis, ln));
+                    xb = make_int4(uni(rl(cb.x, ln)), uni(rl(cb.y, ln)), 0, uni(rl(cb.w, ln)));
+                    if (Dn < kWave) {
+                        px = wl(px, x, Dn);
+                        pvv = wl(pvv, xv, Dn);
+                    } else if (l == 0) {
+                        sPath[Dn] = make_int2(x, xv);
+                    }
+                    return true;
+                };
+                const int ci = pick(0, nc);
+                if (ci < 0 || !advance(fc, ci)) break;
+                if (!ok2) continue;
+                const int nc2 = uni(nc_of(xb.y));
+                if (nc2 == 0) break;
+                const int fc2 = uni(xb.x);
+                const int base = 8 + 8 * ci;  // child ci's group: its children at fc2 + i
+                const int ci2 = pick(base, nc2);
+                if (ci2 < 0 || !advance(fc2, base + ci2)) break;
+                continue;
+            }
+#endif
             // the children's records (lane j = child j), the next level's structure record included
             const bool has = l < nc;
             int4 ca = make_int4(0, 0, 0, 0), cb = ca;
@@ -5858,6 +5999,20 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         out_idx = (Dn == 0) ? uni(sB[0].w) : par_hsx;  // parent->hidden_state_index_x
         out_act = act_of(uni(xb.y));                   // children_action of the last edge
     }
+#ifdef MZ_STAMPS_WALK
+        {
+            const unsigned long long n_ = __builtin_amdgcn_s_memtime();
+            if (twn < 1) tw[1] = n_;
+            if (twn < 2) tw[2] = n_;
+            if (twn < 3) tw[3] = n_;
+            if (twn < 4) tw[4] = n_;
+            if (twn < 5) tw[5] = n_;
+            if (twn < 6) tw[6] = n_;
+            tw[7] = n_;
+            tw[8] = n_;
+        }
+#endif
+#undef MZ_WALK_TOP
         stamp(tp, 3);
     } else {
         // every node's select_child outcome by the four waves (tree_select_prep), then the chase
@@ -6030,8 +6185,13 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #pragma unroll
             for (int q = 0; q < 8; ++q)
                 if (q == k) {
+#ifdef MZ_STAMPS_WALK
+                    d0 = tw[q];
+                    d1 = tw[q + 1];
+#else
                     d0 = ts[q];
                     d1 = ts[q + 1];
+#endif
                 }
             add = (long long)(d1 - d0);
         } else if (MZ_STAMPS && l == MZ_S_STAMPED) {

@@ -3,7 +3,7 @@
 DESIGN.md / README.md / INTEGRATION.md / scripts/README.md quote numbers from `profiles/` and name
 files of this repository.  These checks keep them from drifting: every repository file they name
 exists, README's headline is the committed headline bench line, and DESIGN §5's configuration table
-is the committed reconciliation (`profiles/round5/roofline_reconcile.json`)."""
+is the committed reconciliation (`profiles/round6/roofline_reconcile.json`)."""
 from __future__ import annotations
 
 import json
@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DOCS = ["DESIGN.md", "README.md", "INTEGRATION.md", os.path.join("scripts", "README.md")]
-ROUND = os.path.join(ROOT, "profiles", "round5")
+ROUND = os.path.join(ROOT, "profiles", "round6")
 
 # names of the reference's own sources (in /root/reference, cited by file:line) and of files a
 # document says are gone
@@ -41,7 +41,7 @@ def test_named_files_exist(doc):
             assert os.path.exists(os.path.join(ROUND, "3m_k1", n)), n
             continue
         cands = [n] + [os.path.join(d, n) for d in ("scripts", "mazero_amd", "mazero_amd/csrc", "oracle", "include",
-                                                     "tests", "profiles/round5", "profiles/round4", "profiles/round3",
+                                                     "tests", "profiles/round6", "profiles/round6/ab", "profiles/round5", "profiles/round4", "profiles/round3",
                                                      "profiles")]
         if not any(os.path.exists(os.path.join(ROOT, c)) for c in cands):
             missing.append(n)
@@ -59,7 +59,7 @@ def test_readme_headline_is_the_committed_line():
     assert m, "README's headline sentence"
     assert abs(float(m.group(1)) - b["value"] / 1e6) < 0.05
     cpu = b["cpu_baseline"]["value"]
-    r = re.search(r"([0-9,]+)× the reference ctree on one host core", _read("README.md"))
+    r = re.search(r"([0-9,]+)×\s+the reference ctree on one host core", _read("README.md"))
     assert r and abs(int(r.group(1).replace(",", "")) - b["value"] / cpu) <= 1
 
 
@@ -68,7 +68,7 @@ def test_design_table_is_the_committed_reconciliation():
         rec = json.load(f)
     rows = {}
     text = _read("DESIGN.md")
-    sec = text[text.index("## 5. Measurement (round 5"):text.index("### Round 4 (for the record)")]
+    sec = text[text.index("### Round 6 (`profiles/round6/`)"):text.index("### Round 5 (for the record")]
     for line in sec.splitlines():
         m = re.match(r"\| (3m|2s3z|3s5z_vs_3s6z|27m_vs_30m) (\d+)×(\d+) K=(\d+) \| ([0-9.]+) M \| [^|]+\| ([0-9.]+) µs \|",
                      line)

@@ -289,6 +289,31 @@ def test_trim_caches_releases_destroyed_arenas(gpu_lib):
     assert trim_caches() == 0
 
 
+@pytest.mark.parametrize(
+    "K,S,ties",
+    [(5, 200, True), (5, 200, False), (3, 250, True), (7, 120, True), (7, 120, False), (8, 120, True)],
+    ids=["k5_s200_ties", "k5_s200", "k3_s250_ties", "k7_s120_ties", "k7_s120", "k8_s120_ties"],
+)
+def test_level_walk_two_levels_per_pass(gpu_lib, port_lib, K, S, ties):
+    """The level walk's two-level passes (round 6, k_tree's 1,024-node classes, K <= 7): lanes 0..7
+    score a node's children and lanes 8 + 8g + i child g's children, one segmented max and two
+    ballots resolve both levels.  Uniform policies (`ties`) put a tie list at every level, so both
+    levels read engine words in the pass; K = 8 takes the one-level walk.  Against the port."""
+    from mazero_amd.synthetic import make_search_inputs, run_search
+
+    B, A = 32, 36
+    rng = np.random.default_rng(8080 + 31 * K + S + ties)
+    inp = make_search_inputs(rng, B, A, S, ties=ties)
+    knobs = {}
+    exp = run_search(make_tb(port_lib, inp, K, knobs), inp, K, knobs)
+    tb = make_tb(gpu_lib, inp, K, knobs)
+    assert tb.fused_kernel().startswith("k_tree<1024"), tb.fused_kernel()
+    out, _ = run_fused(tb, to_device(inp), K, knobs)
+    exp = {k: v for k, v in exp.items() if k not in ("root_values_per_sim", "marginal_per_sim")}
+    assert_same(out, exp, f"gpu level walk K={K} S={S} ties={ties} ")
+    assert (out["sampled_visit_count"].sum(axis=1) == S).all()
+
+
 @pytest.mark.parametrize("K,S", [(3, 700), (2, 40)], ids=["k3_s700", "k2_s40"])
 def test_hbm_wave_per_node_backup(gpu_lib, port_lib, K, S, monkeypatch):
     """k_hbm's back-propagation (hbm_node_wave, round 5): one wave per path node, dealt over three
