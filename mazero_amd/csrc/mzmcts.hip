@@ -4605,6 +4605,78 @@ __device__ __forceinline__ void chase_next(int &v, int &cursor, int &x, int &Dn,
         : "vcc", "scc", "memory");
 }
 
+// The level walk's common level in one straight run (round 6, the two-level passes): the tie list of
+// the group of eight at lane `base` from the pass's ballots (tT / tE: the group's bits of the
+// threshold and first-maximum ballots; big: its maximum beats FLOAT_MIN), as pick computes it; then,
+// unless the list has two or more members (a tie: an engine word decides), the node is the root
+// under forced round-robin, its visit count is outside the table, the stream has ended or the path
+// lanes end here -- returned as 1 with nothing changed, pick and advance take the level --, the step
+// to the chosen child: one word if the list is not empty, path lane Dn := {x, visits}, the child's
+// structure record by readlane.  No branch but the exit.
+__device__ __forceinline__ int walk_step8(unsigned tT, unsigned tE, unsigned big, int base, int nc, int fc, int PS,
+                                          int gW, int lim, int &x, int &xv, int &xbx, int &xby, int &xbw,
+                                          int &cursor, int &Dn, int &par_hsx, int &px, int &pvv, int cvis, int cbx,
+                                          int cby, int cbw, int lane) {
+    int slow, t0, t1, r, cnt, ci, ln, lst, a0, a1;
+    asm volatile(
+        "s_ff1_i32_b32 %[r], %[tE]\n\t"
+        "s_lshl_b32 %[t0], -1, %[r]\n\t"
+        "s_cmp_lg_u32 %[big], 0\n\t"
+        "s_cselect_b32 %[t0], %[t0], -1\n\t"
+        "s_and_b32 %[lst], %[tT], %[t0]\n\t"
+        "s_bcnt1_i32_b32 %[cnt], %[lst]\n\t"
+        "s_ff1_i32_b32 %[ci], %[lst]\n\t"
+        "s_max_i32 %[ci], %[ci], 0\n\t"
+        "s_cmp_gt_u32 %[cnt], 1\n\t"
+        "s_cselect_b32 %[slow], 1, 0\n\t"
+        "s_cmp_ge_i32 %[cur], %[gW]\n\t"
+        "s_cselect_b32 %[t0], %[cnt], 0\n\t"
+        "s_or_b32 %[slow], %[slow], %[t0]\n\t"
+        "s_add_i32 %[t0], %[xv], -1\n\t"
+        "s_cmp_ge_u32 %[t0], %[PS]\n\t"
+        "s_cselect_b32 %[t0], 1, 0\n\t"
+        "s_or_b32 %[slow], %[slow], %[t0]\n\t"
+        "s_cmp_eq_u32 %[x], 0\n\t"
+        "s_cselect_b32 %[t0], 1, 0\n\t"
+        "s_cmp_le_i32 %[xv], %[nc]\n\t"
+        "s_cselect_b32 %[t0], %[t0], 0\n\t"
+        "s_or_b32 %[slow], %[slow], %[t0]\n\t"
+        "s_add_i32 %[t1], %[dn], 1\n\t"
+        "s_cmp_ge_i32 %[t1], %[lim]\n\t"
+        "s_cselect_b32 %[t0], 1, 0\n\t"
+        "s_or_b32 %[slow], %[slow], %[t0]\n\t"
+        "s_cmp_lg_u32 %[slow], 0\n\t"
+        "s_cbranch_scc1 .Lws%=_out\n\t"
+        "s_add_i32 %[cur], %[cur], %[cnt]\n\t"
+        "s_mov_b32 %[phs], %[xbw]\n\t"
+        "s_add_i32 %[ln], %[base], %[ci]\n\t"
+        "s_add_i32 %[x], %[fc], %[ci]\n\t"
+        "s_mov_b32 %[dn], %[t1]\n\t"
+        "s_nop 3\n\t"
+        "v_readlane_b32 %[xv], %[cvis], %[ln]\n\t"
+        "v_readlane_b32 %[xbx], %[cbx], %[ln]\n\t"
+        "v_readlane_b32 %[xby], %[cby], %[ln]\n\t"
+        "v_readlane_b32 %[xbw], %[cbw], %[ln]\n\t"
+        "v_cmp_eq_u32_e32 vcc, %[dn], %[lane]\n\t"
+        "v_mov_b32 %[a0], %[x]\n\t"
+        "s_nop 4\n\t"
+        "v_mov_b32 %[a1], %[xv]\n\t"
+        "v_cndmask_b32_e32 %[px], %[px], %[a0], vcc\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e32 %[pvv], %[pvv], %[a1], vcc\n"
+        ".Lws%=_out:\n\t"
+        "s_nop 4"
+        : [slow] "=&s"(slow), [t0] "=&s"(t0), [t1] "=&s"(t1), [r] "=&s"(r), [cnt] "=&s"(cnt), [ci] "=&s"(ci),
+          [ln] "=&s"(ln), [lst] "=&s"(lst), [a0] "=&v"(a0), [a1] "=&v"(a1), [x] "+s"(x), [xv] "+s"(xv),
+          [xbx] "+s"(xbx), [xby] "+s"(xby), [xbw] "+s"(xbw), [cur] "+s"(cursor), [dn] "+s"(Dn),
+          [phs] "+s"(par_hsx), [px] "+v"(px), [pvv] "+v"(pvv)
+        : [tT] "s"(tT), [tE] "s"(tE), [big] "s"(big), [base] "s"(base), [nc] "s"(nc), [fc] "s"(fc), [PS] "s"(PS),
+          [gW] "s"(gW), [lim] "s"(lim), [cvis] "v"(cvis), [cbx] "v"(cbx), [cby] "v"(cby), [cbw] "v"(cbw),
+          [lane] "v"(lane)
+        : "vcc", "scc");
+    return slow;
+}
+
 // the back-propagation waves' exchange records (after barrier (2)): joined error word, min/max and
 // visited-node count (path nodes 1 .. D are visited now, cnode.cpp:431-447)
 // Lane j (1 <= j <= BK <= 7) reads record j, and three DPP steps within each row's first eight lanes
@@ -5761,6 +5833,22 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
 #else
 #define MZ_WALK_TOP() do {} while (0)
 #endif
+#ifdef MZ_STAMPS_SEG
+        // (diagnostic builds with -DMZ_STAMPS_SEG -DMZ_STAMPS_W0: the two-level passes' segments summed
+        // over a tree's passes -- children landed, grandchildren landed, scores + ballots, level 1,
+        // level 2 -- and the pass count, in wave 0's slots)
+        unsigned long long sg0 = 0, sg1 = 0, sg2 = 0, sg3 = 0, sg4 = 0, sgl = 0, sgn = 0;
+#define MZ_SEG(acc)                                                            \
+    do {                                                                        \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                      \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();             \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                      \
+        acc += n_ - sgl;                                                        \
+        sgl = n_;                                                               \
+    } while (0)
+#else
+#define MZ_SEG(acc) do {} while (0)
+#endif
     if (!err) {
         cursor = uni(cursor);
         const bool mm_on = mm_cnt > 0;
@@ -5773,6 +5861,8 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
         int4 xb = uni4(sB[0]);
         int par_hsx = xb.w;
         pvv = wl(pvv, xv, 0);
+        const int lim8 = PS < kWave ? PS : kWave;  // (walk_step8: path lanes)
+        (void)lim8;
         while (true) {
             MZ_WALK_TOP();
             x = uni(x);
@@ -5783,6 +5873,12 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             const int fc = uni(xb.x);
 #ifndef MZ_NO_WALK2
             if (nc <= 7) {
+#ifdef MZ_STAMPS_SEG
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                sgl = __builtin_amdgcn_s_memtime();
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                ++sgn;
+#endif
                 // Two levels per pass (nc <= 7 and every child's nc <= 8): lanes 0..7 hold x's children,
                 // lanes 8 + 8g + i child g's child i.  Each lane scores its node as the one-level pass
                 // below would at that node's level (the scores depend on the node and the launch's
@@ -5811,6 +5907,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                         if constexpr (!kTreeAzLevel<NC>) caz = sAz[n1];
                     }
                 }
+                MZ_SEG(sg0);
                 const int gnc = nc_of(cb.y);
                 const bool ok2 = ballot(!lo && has1 && gnc > 8) == 0ull;
                 const bool has2 = !lo && has1 && sl < gnc;
@@ -5823,6 +5920,7 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                     cfl = sFl[n2];
                     if constexpr (!kTreeAzLevel<NC>) caz = sAz[n2];
                 }
+                MZ_SEG(sg1);
                 if constexpr (kTreeAzLevel<NC>) caz = lo ? az1 : az2;
                 const bool has = lo ? has1 : has2;
                 const int cvis = ca.x + (cfl ? 1 : 0);
@@ -5841,9 +5939,14 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                 Ms = fmaxf(Ms, i2f(dpp<0x4E>(f2i(Ms))));
                 Ms = fmaxf(Ms, i2f(dpp<0x141>(f2i(Ms))));
                 const bool big = Ms > -1000000.0f;
+                const unsigned long long bB = ballot(big);
                 const unsigned long long bE = ballot(has && sc == Ms);
                 const float thr = big ? Ms - 0.000001f : -1000000.0f;
                 const unsigned long long bT = ballot(has && sc >= thr);
+#ifdef MZ_STAMPS_SEG
+                asm volatile("" ::"s"(bT), "s"(bE));
+#endif
+                MZ_SEG(sg2);
                 // one level's select_child from group `base`'s lanes: -1 (err set) ends the walk
                 auto pick = [&](int base, int ncl) -> int {
                     if (x == 0 && xv <= ncl) return xv - 1;  // forced root round-robin (cnode.cpp:398-399)
@@ -5890,15 +5993,42 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
                     }
                     return true;
                 };
+#ifndef MZ_NO_WALKASM
+                // the common case in one straight run (walk_step8); pick and advance otherwise
+                auto step8 = [&](int base, int ncl, int fcl) -> int {  // the chosen child (lane - base), or -1
+                    const unsigned tT = (unsigned)(bT >> base) & 0xffu, tE = (unsigned)(bE >> base) & 0xffu;
+                    const unsigned bg = (unsigned)(bB >> base) & 1u;
+                    if (walk_step8(tT, tE, bg, base, ncl, fcl, PS, gW, lim8, x, xv, xb.x, xb.y, xb.w, cursor, Dn,
+                                   par_hsx, px, pvv, cvis, cb.x, cb.y, cb.w, l))
+                        return -1;
+                    nscored += ncl;
+                    return x - fcl;  // (x = fcl + the child)
+                };
+                int ci = step8(0, nc, fc);
+                if (ci < 0) {
+                    ci = pick(0, nc);
+                    if (ci < 0 || !advance(fc, ci)) break;
+                }
+#else
                 const int ci = pick(0, nc);
                 if (ci < 0 || !advance(fc, ci)) break;
+#endif
+                MZ_SEG(sg3);
                 if (!ok2) continue;
                 const int nc2 = uni(nc_of(xb.y));
                 if (nc2 == 0) break;
                 const int fc2 = uni(xb.x);
                 const int base = 8 + 8 * ci;  // child ci's group: its children at fc2 + i
+#ifndef MZ_NO_WALKASM
+                if (step8(base, nc2, fc2) < 0) {
+                    const int ci2 = pick(base, nc2);
+                    if (ci2 < 0 || !advance(fc2, base + ci2)) break;
+                }
+#else
                 const int ci2 = pick(base, nc2);
                 if (ci2 < 0 || !advance(fc2, base + ci2)) break;
+#endif
+                MZ_SEG(sg4);
                 continue;
             }
 #endif
@@ -6012,6 +6142,18 @@ __global__ __launch_bounds__(kTreeWavesN<NC> * 64) void k_tree(char *base, const
             tw[8] = n_;
         }
 #endif
+#ifdef MZ_STAMPS_SEG
+        tw[0] = 0;
+        tw[1] = sg0;
+        tw[2] = tw[1] + sg1;
+        tw[3] = tw[2] + sg2;
+        tw[4] = tw[3] + sg3;
+        tw[5] = tw[4] + sg4;
+        tw[6] = tw[5];
+        tw[7] = tw[6] + sgn;
+        tw[8] = tw[7];
+#endif
+#undef MZ_SEG
 #undef MZ_WALK_TOP
         stamp(tp, 3);
     } else {
